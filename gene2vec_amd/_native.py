@@ -1,0 +1,118 @@
+"""ctypes binding of ``libg2v.so`` (C ABI in ``include/g2v.h``).
+
+There is no fallback: if the library is missing or fails to load, every
+entry point raises ``NativeLibraryError``.  Build it with
+``python -m gene2vec_amd.build`` (or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libg2v.so")
+
+G2V_OK = 0
+G2V_EINVAL = -1
+G2V_EHIP = -2
+G2V_ENOMEM = -3
+G2V_ESTATE = -4
+G2V_ERANGE = -5
+
+MODE_HOGWILD = 0
+MODE_SEQUENTIAL = 1
+MODE_MINIBATCH = 2
+FLAG_TIMING = 0x100
+CORPUS_DEVICE = 0x1
+BATCH_WORDS = 10000
+MAX_DIM = 512
+SUPPORTED_NEGATIVE = (1, 2, 3, 5, 10, 15, 20)
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class G2VError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"g2v error {code}: {msg}")
+        self.code = code
+
+
+class Stats(C.Structure):
+    _fields_ = [("raw_words", C.c_int64), ("effective_words", C.c_int64),
+                ("examples", C.c_int64), ("jobs", C.c_int64), ("launches", C.c_int64),
+                ("sgns_kernel_ms", C.c_double), ("sample_kernel_ms", C.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_vp = C.c_void_p
+_i32 = C.c_int32
+_i64 = C.c_int64
+_u32 = C.c_uint32
+_f32 = C.c_float
+_f64 = C.c_double
+
+# name -> (restype, argtypes); every symbol include/g2v.h declares
+SIGNATURES = {
+    "g2v_last_error": (C.c_char_p, []),
+    "g2v_abi_version": (C.c_int, []),
+    "g2v_create": (C.c_int, [C.c_int, _i32, _i32, _i32, _i32, C.POINTER(_vp)]),
+    "g2v_destroy": (C.c_int, [_vp]),
+    "g2v_set_stream": (C.c_int, [_vp, _vp]),
+    "g2v_row_stride": (C.c_int, [_vp, C.POINTER(_i64)]),
+    "g2v_set_vocab": (C.c_int, [_vp, _vp, _f64, _f64, _vp, _vp]),
+    "g2v_bind_tables": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "g2v_set_weights": (C.c_int, [_vp, _vp, _vp, _vp]),
+    "g2v_get_weights": (C.c_int, [_vp, _vp, _vp]),
+    "g2v_set_corpus": (C.c_int, [_vp, _vp, _i64, _vp, _i64, _i64, _u32]),
+    "g2v_plan_jobs": (C.c_int, [_vp, _i64, _i64, _i64, _vp, _i64, C.POINTER(_i64)]),
+    "g2v_train": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _u32]),
+    "g2v_sgns_step_explicit": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _f32, _u32]),
+    "g2v_debug_sample": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, C.POINTER(_i64)]),
+    "g2v_sync": (C.c_int, [_vp]),
+    "g2v_read_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
+    "g2v_seeded_vectors": (C.c_int, [_vp, _i64, _i32, _vp]),
+    "g2v_count_ids": (C.c_int, [_vp, _i64, _i32, _vp, _vp]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libg2v.so once; raise loudly when it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} is missing: build it with `python -m gene2vec_amd.build` "
+            "(the SGNS path has no CPU fallback)")
+    try:
+        L = C.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover - depends on the ROCm runtime
+        raise NativeLibraryError(f"failed to load {LIB_PATH}: {e}") from e
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    if L.g2v_abi_version() != 1:
+        raise NativeLibraryError("libg2v ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != G2V_OK:
+        msg = lib().g2v_last_error()
+        raise G2VError(rc, msg.decode() if msg else "")
+    return rc
+
+
+def ptr(a):
+    """data pointer of a numpy array (or None)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.c_void_p)

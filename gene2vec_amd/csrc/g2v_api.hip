@@ -1,0 +1,745 @@
+// g2v_api.hip -- C ABI of libg2v.so (declared in include/g2v.h).
+//
+// Owns the device state that gensim keeps in the Word2Vec model object
+// ([ext] wv.vectors, trainables.syn1neg, trainables.vectors_lockf,
+// vocabulary.cum_table, per-word sample_int) and replaces the per-job hook
+// train_batch_sg that gensim's worker threads call (src/gene2vec.py:70,87).
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "g2v.h"
+#include "g2v_internal.h"
+
+using namespace g2v;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(x)                                                                          \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(G2V_EHIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                               \
+  } while (0)
+
+#define REQUIRE(cond, code, ...)                \
+  do {                                                \
+    if (!(cond)) return fail((code), __VA_ARGS__);    \
+  } while (0)
+
+template <typename T>
+int dev_alloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  if (e != hipSuccess)
+    return fail(G2V_ENOMEM, "hipMalloc(%zu bytes) failed: %s", n * sizeof(T), hipGetErrorString(e));
+  return G2V_OK;
+}
+
+template <typename T>
+void dev_free(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+// grow a device buffer (contents discarded); caller guarantees no in-flight use
+// (stream-ordered: we synchronise the stream before freeing)
+template <typename T>
+int dev_reserve(hipStream_t st, T** p, int64_t* cap, int64_t need) {
+  if (need <= *cap && *p) return G2V_OK;
+  if (*p) {
+    HIPCHK(hipStreamSynchronize(st));
+    dev_free(*p);
+  }
+  int64_t n = std::max<int64_t>(need, *cap + *cap / 2);
+  int rc = dev_alloc(p, (size_t)n);
+  if (rc) {
+    *cap = 0;
+    return rc;
+  }
+  *cap = n;
+  return G2V_OK;
+}
+
+}  // namespace
+
+struct g2v_ctx {
+  int device = 0;
+  int32_t V = 0, D = 0, K = 0, window = 1;
+  int nv = 1, nvec = 0, rec_stride = 0;
+  int64_t ld = 0;
+  int cus = 0, sgns_grid = 0;
+  hipStream_t own_stream = nullptr, stream = nullptr;
+
+  float *own0 = nullptr, *own1 = nullptr;  // context-owned tables
+  float *syn0 = nullptr, *syn1 = nullptr;  // active tables (owned or borrowed)
+  float* lockf = nullptr;
+  float* exp_table = nullptr;
+  uint64_t* jump = nullptr;  // 4 x kJumpTab
+  uint32_t *cum = nullptr, *sample_int = nullptr;
+  int32_t* bkt = nullptr;
+  int64_t* d_counts = nullptr;
+  double* d_cpow = nullptr;
+  int sample_on = 0;
+  bool vocab_ready = false, weights_ready = false;
+
+  // corpus
+  const int32_t* tok = nullptr;
+  const int64_t* sent_off = nullptr;
+  int32_t* own_tok = nullptr;
+  int64_t* own_off = nullptr;
+  int64_t n_tok = 0, n_sent = 0, sent_len = 0;
+  std::vector<int64_t> h_sent_off;  // host copy (host-provided CSR only)
+  bool corpus_ready = false;
+
+  // job tables
+  int64_t job_cap = 0;
+  int64_t* d_job_sent = nullptr;
+  float* d_job_alpha = nullptr;
+  uint64_t* d_job_seed = nullptr;
+  int64_t job_alpha_cap = 0, job_seed_cap = 0;
+  void* h_stage = nullptr;
+  size_t h_stage_cap = 0;
+  hipEvent_t stage_ev = nullptr;
+  bool stage_pending = false;
+
+  // per-segment workspace
+  int64_t seg_jobs = 1024;
+  int64_t nex_cap = 0, exoff_cap = 0, rec_cap = 0;
+  int32_t* d_job_nex = nullptr;
+  int64_t* d_job_exoff = nullptr;
+  int32_t* d_rec = nullptr;
+
+  // explicit-step scratch
+  int64_t ex_cap = 0, snap0_cap = 0, snap1_cap = 0;
+  int32_t* d_ex = nullptr;  // center | input | negs
+  float *snap0 = nullptr, *snap1 = nullptr;
+
+  // counters: [0] effective words, [1] examples, [2] raw words
+  unsigned long long* d_counters = nullptr;
+  int64_t jobs = 0, launches = 0;
+
+  // timing
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> t_sgns, t_samp;
+};
+
+static int ctx_event(g2v_ctx* c, hipEvent_t* out) {
+  if (c->ev_used == c->ev_pool.size()) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    c->ev_pool.push_back(e);
+  }
+  *out = c->ev_pool[c->ev_used++];
+  return G2V_OK;
+}
+
+static int set_dev(g2v_ctx* c) {
+  REQUIRE(c != nullptr, G2V_EINVAL, "null context");
+  HIPCHK(hipSetDevice(c->device));
+  return G2V_OK;
+}
+
+extern "C" {
+
+const char* g2v_last_error(void) { return g_err.c_str(); }
+
+int g2v_abi_version(void) { return G2V_ABI_VERSION; }
+
+int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t negative,
+               int32_t window, g2v_ctx** out) {
+  REQUIRE(out != nullptr, G2V_EINVAL, "out is null");
+  *out = nullptr;
+  REQUIRE(vocab_size > 0, G2V_EINVAL, "vocab_size must be > 0 (got %d)", vocab_size);
+  REQUIRE(vector_size >= 1 && vector_size <= G2V_MAX_DIM, G2V_EINVAL,
+          "vector_size must be in [1, %d] (got %d)", G2V_MAX_DIM, vector_size);
+  REQUIRE(window == 1, G2V_EINVAL,
+          "window=%d: only window=1 (src/gene2vec.py:62) is implemented", window);
+  const int nvec = (vector_size + 3) / 4;
+  const int nv = nvec <= 64 ? 1 : 2;
+  REQUIRE(sgns_supported(negative, nv), G2V_EINVAL,
+          "negative=%d not compiled (supported: 1,2,3,5,10,15,20)", negative);
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  REQUIRE(device >= 0 && device < ndev, G2V_EINVAL, "device %d out of range (%d devices)", device,
+          ndev);
+  HIPCHK(hipSetDevice(device));
+
+  g2v_ctx* c = new (std::nothrow) g2v_ctx();
+  REQUIRE(c != nullptr, G2V_ENOMEM, "context allocation failed");
+  c->device = device;
+  c->V = vocab_size;
+  c->D = vector_size;
+  c->K = negative;
+  c->window = window;
+  c->nvec = nvec;
+  c->nv = nv;
+  c->ld = ((int64_t)vector_size + 31) / 32 * 32;  // 128-B aligned rows
+  c->rec_stride = (3 + negative + 3) / 4 * 4;      // 16-B aligned records
+  if (const char* s = getenv("G2V_SEG_JOBS")) c->seg_jobs = std::max(1, atoi(s));
+
+  int rc = G2V_OK;
+  auto bail = [&](int r) {
+    g2v_destroy(c);
+    return r;
+  };
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+    return bail(fail(G2V_EHIP, "hipGetDeviceProperties failed"));
+  c->cus = prop.multiProcessorCount;
+  c->sgns_grid = c->cus * sgns_blocks_per_cu(negative, nv);
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(G2V_EHIP, "hipStreamCreate failed"));
+  c->stream = c->own_stream;
+  if (hipEventCreateWithFlags(&c->stage_ev, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(G2V_EHIP, "hipEventCreate failed"));
+
+  const size_t tab = (size_t)c->V * (size_t)c->ld;
+  if ((rc = dev_alloc(&c->own0, tab)) || (rc = dev_alloc(&c->own1, tab)) ||
+      (rc = dev_alloc(&c->lockf, (size_t)c->V)) || (rc = dev_alloc(&c->exp_table, kExpTableSize)) ||
+      (rc = dev_alloc(&c->jump, 4 * (size_t)kJumpTab)) || (rc = dev_alloc(&c->cum, (size_t)c->V)) ||
+      (rc = dev_alloc(&c->sample_int, (size_t)c->V)) ||
+      (rc = dev_alloc(&c->bkt, (size_t)kBuckets + 1)) ||
+      (rc = dev_alloc(&c->d_counts, (size_t)c->V)) || (rc = dev_alloc(&c->d_cpow, (size_t)c->V)) ||
+      (rc = dev_alloc(&c->d_counters, 4)))
+    return bail(rc);
+  c->syn0 = c->own0;
+  c->syn1 = c->own1;
+
+  // constant tables: sigmoid LUT ([ext] init()) and LCG jump tables, built on host
+  float lut[kExpTableSize];
+  for (int i = 0; i < kExpTableSize; ++i) {
+    const float x = ((float)i / (float)kExpTableSize * 2 - 1) * kMaxExp;
+    const float e = (float)exp((double)x);
+    lut[i] = e / (e + 1);
+  }
+  std::vector<uint64_t> jt(4 * (size_t)kJumpTab);
+  lcg_jump_tables(jt.data(), jt.data() + kJumpTab, jt.data() + 2 * kJumpTab,
+                  jt.data() + 3 * kJumpTab);
+  if (hipMemcpy(c->exp_table, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->jump, jt.data(), jt.size() * sizeof(uint64_t), hipMemcpyHostToDevice) !=
+          hipSuccess ||
+      hipMemset(c->own0, 0, tab * sizeof(float)) != hipSuccess ||
+      hipMemset(c->own1, 0, tab * sizeof(float)) != hipSuccess ||
+      hipMemset(c->d_counters, 0, 4 * sizeof(unsigned long long)) != hipSuccess)
+    return bail(fail(G2V_EHIP, "initial upload failed"));
+  std::vector<float> ones((size_t)c->V, 1.0f);
+  if (hipMemcpy(c->lockf, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice) !=
+      hipSuccess)
+    return bail(fail(G2V_EHIP, "lockf upload failed"));
+  *out = c;
+  return G2V_OK;
+}
+
+int g2v_destroy(g2v_ctx* c) {
+  if (!c) return G2V_OK;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  dev_free(c->own0);
+  dev_free(c->own1);
+  dev_free(c->lockf);
+  dev_free(c->exp_table);
+  dev_free(c->jump);
+  dev_free(c->cum);
+  dev_free(c->sample_int);
+  dev_free(c->bkt);
+  dev_free(c->d_counts);
+  dev_free(c->d_cpow);
+  dev_free(c->own_tok);
+  dev_free(c->own_off);
+  dev_free(c->d_job_sent);
+  dev_free(c->d_job_alpha);
+  dev_free(c->d_job_seed);
+  dev_free(c->d_job_nex);
+  dev_free(c->d_job_exoff);
+  dev_free(c->d_rec);
+  dev_free(c->d_ex);
+  dev_free(c->snap0);
+  dev_free(c->snap1);
+  dev_free(c->d_counters);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return G2V_OK;
+}
+
+int g2v_set_stream(g2v_ctx* c, void* s) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  c->stream = s ? (hipStream_t)s : c->own_stream;
+  return G2V_OK;
+}
+
+int g2v_row_stride(g2v_ctx* c, int64_t* ld_out) {
+  REQUIRE(c && ld_out, G2V_EINVAL, "null argument");
+  *ld_out = c->ld;
+  return G2V_OK;
+}
+
+int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_exponent,
+                  uint32_t* cum_out, uint32_t* sample_int_out) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(counts != nullptr, G2V_EINVAL, "counts is null");
+  REQUIRE(sample >= 0.0, G2V_EINVAL, "sample must be >= 0");
+  for (int32_t i = 0; i < c->V; ++i)
+    REQUIRE(counts[i] > 0, G2V_EINVAL, "counts[%d] = %lld must be > 0", i, (long long)counts[i]);
+  HIPCHK(hipMemcpyAsync(c->d_counts, counts, sizeof(int64_t) * c->V, hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(launch_vocab(c->d_counts, c->d_cpow, c->V, ns_exponent, sample, c->cum, c->sample_int,
+                      c->bkt, c->stream));
+  c->sample_on = sample != 0.0;
+  if (cum_out)
+    HIPCHK(hipMemcpyAsync(cum_out, c->cum, sizeof(uint32_t) * c->V, hipMemcpyDeviceToHost,
+                          c->stream));
+  if (sample_int_out)
+    HIPCHK(hipMemcpyAsync(sample_int_out, c->sample_int, sizeof(uint32_t) * c->V,
+                          hipMemcpyDeviceToHost, c->stream));
+  if (cum_out || sample_int_out) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (cum_out && cum_out[c->V - 1] != 2147483647u)
+      return fail(G2V_EINVAL, "cum_table[-1] = %u != 2**31-1", cum_out[c->V - 1]);
+  }
+  c->vocab_ready = true;
+  return G2V_OK;
+}
+
+int g2v_bind_tables(g2v_ctx* c, float* s0, float* s1, int64_t ld) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  if (!s0 && !s1) {
+    c->syn0 = c->own0;
+    c->syn1 = c->own1;
+    c->ld = ((int64_t)c->D + 31) / 32 * 32;
+    return G2V_OK;
+  }
+  REQUIRE(s0 && s1, G2V_EINVAL, "bind both tables or neither");
+  REQUIRE(ld >= c->D && ld % 4 == 0, G2V_EINVAL, "ld=%lld must be >= D=%d and a multiple of 4",
+          (long long)ld, c->D);
+  REQUIRE(((uintptr_t)s0 % 16) == 0 && ((uintptr_t)s1 % 16) == 0, G2V_EINVAL,
+          "tables must be 16-byte aligned");
+  c->syn0 = s0;
+  c->syn1 = s1;
+  c->ld = ld;
+  c->weights_ready = true;
+  return G2V_OK;
+}
+
+int g2v_set_weights(g2v_ctx* c, const float* s0, const float* s1, const float* lockf) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  const size_t row = sizeof(float) * (size_t)c->D, pitch = sizeof(float) * (size_t)c->ld;
+  if (s0) {
+    HIPCHK(hipMemsetAsync(c->syn0, 0, pitch * c->V, c->stream));
+    HIPCHK(hipMemcpy2DAsync(c->syn0, pitch, s0, row, row, c->V, hipMemcpyHostToDevice, c->stream));
+  }
+  if (s1) {
+    HIPCHK(hipMemsetAsync(c->syn1, 0, pitch * c->V, c->stream));
+    HIPCHK(hipMemcpy2DAsync(c->syn1, pitch, s1, row, row, c->V, hipMemcpyHostToDevice, c->stream));
+  }
+  if (lockf)
+    HIPCHK(hipMemcpyAsync(c->lockf, lockf, sizeof(float) * c->V, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));  // host buffers are only borrowed for the call
+  c->weights_ready = true;
+  return G2V_OK;
+}
+
+int g2v_get_weights(g2v_ctx* c, float* s0, float* s1) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  const size_t row = sizeof(float) * (size_t)c->D, pitch = sizeof(float) * (size_t)c->ld;
+  if (s0)
+    HIPCHK(hipMemcpy2DAsync(s0, row, c->syn0, pitch, row, c->V, hipMemcpyDeviceToHost, c->stream));
+  if (s1)
+    HIPCHK(hipMemcpy2DAsync(s1, row, c->syn1, pitch, row, c->V, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return G2V_OK;
+}
+
+int g2v_set_corpus(g2v_ctx* c, const int32_t* tokens, int64_t n_tokens, const int64_t* sent_off,
+                   int64_t n_sent, int64_t sent_len, uint32_t flags) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(n_tokens >= 0 && n_sent >= 0, G2V_EINVAL, "negative sizes");
+  REQUIRE(tokens || n_tokens == 0, G2V_EINVAL, "tokens is null");
+  REQUIRE(sent_len > 0 || sent_off, G2V_EINVAL, "need sent_off or sent_len > 0");
+  if (sent_len > 0)
+    REQUIRE(n_tokens == n_sent * sent_len, G2V_EINVAL,
+            "n_tokens=%lld != n_sent*sent_len=%lld", (long long)n_tokens,
+            (long long)(n_sent * sent_len));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  dev_free(c->own_tok);
+  dev_free(c->own_off);
+  c->h_sent_off.clear();
+  c->n_tok = n_tokens;
+  c->n_sent = n_sent;
+  c->sent_len = sent_len;
+  if (flags & G2V_CORPUS_DEVICE) {
+    c->tok = tokens;
+    c->sent_off = sent_len > 0 ? nullptr : sent_off;
+  } else {
+    if ((rc = dev_alloc(&c->own_tok, (size_t)n_tokens))) return rc;
+    HIPCHK(hipMemcpy(c->own_tok, tokens, sizeof(int32_t) * n_tokens, hipMemcpyHostToDevice));
+    c->tok = c->own_tok;
+    if (sent_len > 0) {
+      c->sent_off = nullptr;
+    } else {
+      REQUIRE(sent_off[0] == 0 && sent_off[n_sent] == n_tokens, G2V_EINVAL,
+              "sent_off must start at 0 and end at n_tokens");
+      if ((rc = dev_alloc(&c->own_off, (size_t)n_sent + 1))) return rc;
+      HIPCHK(hipMemcpy(c->own_off, sent_off, sizeof(int64_t) * (n_sent + 1),
+                       hipMemcpyHostToDevice));
+      c->sent_off = c->own_off;
+      c->h_sent_off.assign(sent_off, sent_off + n_sent + 1);
+    }
+  }
+  c->corpus_ready = true;
+  return G2V_OK;
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// training driver
+// ---------------------------------------------------------------------------
+static int64_t tokens_between(const g2v_ctx* c, int64_t s0, int64_t s1) {
+  if (c->sent_len > 0) return (s1 - s0) * c->sent_len;
+  if (!c->h_sent_off.empty()) return c->h_sent_off[s1] - c->h_sent_off[s0];
+  return -1;  // unknown on host (device-borrowed CSR)
+}
+
+// stage job tables through pinned memory so the copy is truly asynchronous
+static int upload_jobs(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha,
+                       const uint64_t* job_seed, int64_t n_jobs) {
+  int rc;
+  if ((rc = dev_reserve(c->stream, &c->d_job_sent, &c->job_cap, n_jobs + 1))) return rc;
+  if ((rc = dev_reserve(c->stream, &c->d_job_alpha, &c->job_alpha_cap, std::max<int64_t>(n_jobs, 1))))
+    return rc;
+  if ((rc = dev_reserve(c->stream, &c->d_job_seed, &c->job_seed_cap, std::max<int64_t>(n_jobs, 1))))
+    return rc;
+  const size_t b_sent = sizeof(int64_t) * (n_jobs + 1), b_alpha = sizeof(float) * n_jobs,
+               b_seed = sizeof(uint64_t) * n_jobs;
+  const size_t need = b_sent + b_seed + b_alpha + 64;
+  if (c->stage_pending) {
+    HIPCHK(hipEventSynchronize(c->stage_ev));
+    c->stage_pending = false;
+  }
+  if (need > c->h_stage_cap) {
+    if (c->h_stage) HIPCHK(hipHostFree(c->h_stage));
+    c->h_stage = nullptr;
+    HIPCHK(hipHostMalloc(&c->h_stage, need * 2, hipHostMallocDefault));
+    c->h_stage_cap = need * 2;
+  }
+  char* p = (char*)c->h_stage;
+  memcpy(p, job_sent, b_sent);
+  memcpy(p + b_sent, job_seed, b_seed);
+  if (job_alpha) memcpy(p + b_sent + b_seed, job_alpha, b_alpha);
+  else memset(p + b_sent + b_seed, 0, b_alpha);
+  HIPCHK(hipMemcpyAsync(c->d_job_sent, p, b_sent, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_job_seed, p + b_sent, b_seed, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_job_alpha, p + b_sent + b_seed, b_alpha, hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipEventRecord(c->stage_ev, c->stream));
+  c->stage_pending = true;
+  return G2V_OK;
+}
+
+static int check_jobs(const g2v_ctx* c, const int64_t* job_sent, int64_t n_jobs) {
+  REQUIRE(n_jobs >= 0, G2V_EINVAL, "n_jobs < 0");
+  REQUIRE(job_sent != nullptr, G2V_EINVAL, "job_sent is null");
+  for (int64_t j = 0; j < n_jobs; ++j) {
+    REQUIRE(job_sent[j] >= 0 && job_sent[j] <= job_sent[j + 1] && job_sent[j + 1] <= c->n_sent,
+            G2V_EINVAL, "job %lld sentence range [%lld, %lld) invalid (n_sent=%lld)",
+            (long long)j, (long long)job_sent[j], (long long)job_sent[j + 1],
+            (long long)c->n_sent);
+    const int64_t nt = tokens_between(c, job_sent[j], job_sent[j + 1]);
+    REQUIRE(nt <= kBatchWords, G2V_ERANGE, "job %lld holds %lld raw words > batch_words %d",
+            (long long)j, (long long)nt, kBatchWords);
+  }
+  return G2V_OK;
+}
+
+// count -> scan -> write records for jobs [j0, j0+nj); returns the record buffer
+static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing) {
+  int rc;
+  if ((rc = dev_reserve(c->stream, &c->d_job_nex, &c->nex_cap, nj))) return rc;
+  if ((rc = dev_reserve(c->stream, &c->d_job_exoff, &c->exoff_cap, nj + 1))) return rc;
+  // examples per job <= 2 * raw words (window 1)
+  int64_t max_ex = nj * 2 * (int64_t)kBatchWords;
+  // tighter bound when the token count is known on host
+  // (job_sent lives in pinned staging, still valid: read it from there)
+  const int64_t* hjs = (const int64_t*)c->h_stage;
+  const int64_t tk = tokens_between(c, hjs[j0], hjs[j0 + nj]);
+  if (tk >= 0) max_ex = std::max<int64_t>(2 * tk, 1);
+  if ((rc = dev_reserve(c->stream, &c->d_rec, &c->rec_cap, max_ex * c->rec_stride))) return rc;
+
+  SampleArgs a{};
+  a.tok = c->tok;
+  a.sent_off = c->sent_off;
+  a.sent_len = c->sent_len;
+  a.job_sent = c->d_job_sent;
+  a.job_seed = c->d_job_seed;
+  a.job_alpha = c->d_job_alpha;
+  a.job0 = j0;
+  a.sample_int = c->sample_int;
+  a.sample_on = c->sample_on;
+  a.cum = c->cum;
+  a.bkt = c->bkt;
+  a.V = c->V;
+  a.jump = LcgJump{c->jump, c->jump + kJumpTab, c->jump + 2 * kJumpTab, c->jump + 3 * kJumpTab};
+  a.K = c->K;
+  a.rec_stride = c->rec_stride;
+  a.job_nex = c->d_job_nex;
+  a.job_exoff = c->d_job_exoff;
+  a.rec = c->d_rec;
+  a.counters = c->d_counters;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (timing) {
+    if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
+    HIPCHK(hipEventRecord(e0, c->stream));
+  }
+  HIPCHK(launch_job_sample(false, a, nj, c->stream));
+  HIPCHK(launch_scan_jobs(c->d_job_nex, nj, c->d_job_exoff, c->d_counters + 1, c->stream));
+  HIPCHK(launch_job_sample(true, a, nj, c->stream));
+  if (timing) {
+    HIPCHK(hipEventRecord(e1, c->stream));
+    c->t_samp.emplace_back(e0, e1);
+  }
+  return G2V_OK;
+}
+
+static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool timing,
+                    const float* rd0, const float* rd1) {
+  SgnsArgs s{};
+  s.rec = c->d_rec;
+  s.rec_stride = c->rec_stride;
+  s.n_examples = n_examples_dev;
+  s.rd0 = rd0;
+  s.rd1 = rd1;
+  s.wr0 = c->syn0;
+  s.wr1 = c->syn1;
+  s.lockf = c->lockf;
+  s.ld = c->ld;
+  s.nvec = c->nvec;
+  s.exp_table = c->exp_table;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc;
+  if (timing) {
+    if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
+    HIPCHK(hipEventRecord(e0, c->stream));
+  }
+  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->sgns_grid, c->stream));
+  if (timing) {
+    HIPCHK(hipEventRecord(e1, c->stream));
+    c->t_sgns.emplace_back(e0, e1);
+  }
+  c->launches++;
+  return G2V_OK;
+}
+
+extern "C" {
+
+int g2v_plan_jobs(const int64_t* sent_off, int64_t n_sent, int64_t sent_len, int64_t batch_words,
+                  int64_t* job_sent, int64_t cap, int64_t* n_jobs_out) {
+  REQUIRE(n_jobs_out != nullptr, G2V_EINVAL, "n_jobs_out is null");
+  REQUIRE(n_sent >= 0 && batch_words > 0, G2V_EINVAL, "bad sizes");
+  REQUIRE(sent_len > 0 || sent_off, G2V_EINVAL, "need sent_off or sent_len > 0");
+  // [ext] _job_producer: `if batch_size + len <= batch_words: append else: push`
+  int64_t nj = 0, size = 0, start = 0;
+  auto emit = [&](int64_t s) {
+    if (job_sent && nj < cap) job_sent[nj] = s;
+    ++nj;
+  };
+  for (int64_t i = 0; i < n_sent; ++i) {
+    const int64_t ln = sent_len > 0 ? sent_len : sent_off[i + 1] - sent_off[i];
+    REQUIRE(ln <= batch_words, G2V_ERANGE,
+            "sentence %lld has %lld tokens > batch_words %lld (unsupported)", (long long)i,
+            (long long)ln, (long long)batch_words);
+    if (size + ln <= batch_words) {
+      size += ln;
+    } else {
+      emit(start);
+      start = i;
+      size = ln;
+    }
+  }
+  if (n_sent > start) emit(start);
+  if (job_sent && nj < cap) job_sent[nj] = n_sent;
+  *n_jobs_out = nj;
+  if (job_sent && cap < nj + 1)
+    return fail(G2V_ERANGE, "job_sent capacity %lld < %lld", (long long)cap, (long long)(nj + 1));
+  return G2V_OK;
+}
+
+int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const uint64_t* job_seed,
+              int64_t n_jobs, uint32_t flags) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(c->vocab_ready, G2V_ESTATE, "g2v_set_vocab must precede g2v_train");
+  REQUIRE(c->corpus_ready, G2V_ESTATE, "g2v_set_corpus must precede g2v_train");
+  REQUIRE(job_alpha && job_seed, G2V_EINVAL, "job_alpha / job_seed is null");
+  const int mode = (int)(flags & G2V_MODE_MASK);
+  REQUIRE(mode == kModeHogwild || mode == kModeSequential, G2V_EINVAL,
+          "g2v_train mode must be HOGWILD or SEQUENTIAL");
+  if ((rc = check_jobs(c, job_sent, n_jobs))) return rc;
+  if (n_jobs == 0) return G2V_OK;
+  const bool timing = flags & G2V_FLAG_TIMING;
+  if ((rc = upload_jobs(c, job_sent, job_alpha, job_seed, n_jobs))) return rc;
+  for (int64_t j0 = 0; j0 < n_jobs; j0 += c->seg_jobs) {
+    const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
+    if ((rc = sample_segment(c, j0, nj, timing))) return rc;
+    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, c->syn0, c->syn1))) return rc;
+  }
+  c->jobs += n_jobs;
+  return G2V_OK;
+}
+
+int g2v_debug_sample(g2v_ctx* c, const int64_t* job_sent, const uint64_t* job_seed, int64_t n_jobs,
+                     int32_t* rec_out, int64_t cap, int64_t* n_out) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(c->vocab_ready && c->corpus_ready, G2V_ESTATE, "vocab and corpus required");
+  REQUIRE(n_out != nullptr && job_seed != nullptr, G2V_EINVAL, "null argument");
+  if ((rc = check_jobs(c, job_sent, n_jobs))) return rc;
+  *n_out = 0;
+  if (n_jobs == 0) return G2V_OK;
+  if ((rc = upload_jobs(c, job_sent, nullptr, job_seed, n_jobs))) return rc;
+  int64_t total = 0;
+  const int K2 = c->K + 2;
+  std::vector<int32_t> tmp;
+  for (int64_t j0 = 0; j0 < n_jobs; j0 += c->seg_jobs) {
+    const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
+    if ((rc = sample_segment(c, j0, nj, false))) return rc;
+    int64_t ne = 0;
+    HIPCHK(hipMemcpyAsync(&ne, c->d_job_exoff + nj, sizeof ne, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    tmp.resize((size_t)std::max<int64_t>(ne, 1) * c->rec_stride);
+    if (ne)
+      HIPCHK(hipMemcpy(tmp.data(), c->d_rec, sizeof(int32_t) * ne * c->rec_stride,
+                       hipMemcpyDeviceToHost));
+    for (int64_t i = 0; i < ne; ++i) {
+      if (rec_out && total + i < cap) {
+        int32_t* o = rec_out + (total + i) * K2;
+        const int32_t* r = tmp.data() + i * c->rec_stride;
+        o[0] = r[0];
+        o[1] = r[1];
+        for (int d = 0; d < c->K; ++d) o[2 + d] = r[3 + d];
+      }
+    }
+    total += ne;
+  }
+  *n_out = total;
+  return G2V_OK;
+}
+
+int g2v_sgns_step_explicit(g2v_ctx* c, const int32_t* center, const int32_t* input,
+                           const int32_t* negs, int64_t n, float alpha, uint32_t flags) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(center && input && negs, G2V_EINVAL, "null argument");
+  REQUIRE(n >= 0, G2V_EINVAL, "n < 0");
+  const int mode = (int)(flags & G2V_MODE_MASK);
+  REQUIRE(mode <= kModeMinibatch, G2V_EINVAL, "bad mode %d", mode);
+  for (int64_t i = 0; i < n; ++i) {
+    REQUIRE(center[i] >= 0 && center[i] < c->V && input[i] >= 0 && input[i] < c->V, G2V_EINVAL,
+            "example %lld index out of range", (long long)i);
+    for (int d = 0; d < c->K; ++d)
+      REQUIRE(negs[i * c->K + d] >= -1 && negs[i * c->K + d] < c->V, G2V_EINVAL,
+              "example %lld negative %d out of range", (long long)i, d);
+  }
+  if (n == 0) return G2V_OK;
+  const int64_t words = n * (2 + c->K);
+  if ((rc = dev_reserve(c->stream, &c->d_ex, &c->ex_cap, words))) return rc;
+  if ((rc = dev_reserve(c->stream, &c->d_rec, &c->rec_cap, n * c->rec_stride))) return rc;
+  if ((rc = dev_reserve(c->stream, &c->d_job_exoff, &c->exoff_cap, 1))) return rc;
+  HIPCHK(hipMemcpyAsync(c->d_ex, center, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_ex + n, input, sizeof(int32_t) * n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_ex + 2 * n, negs, sizeof(int32_t) * n * c->K, hipMemcpyHostToDevice,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(c->d_job_exoff, &n, sizeof n, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(launch_explicit_records(c->d_ex, c->d_ex + n, c->d_ex + 2 * n, n, c->K, alpha,
+                                 c->rec_stride, c->d_rec, c->stream));
+  const float* rd0 = c->syn0;
+  const float* rd1 = c->syn1;
+  if (mode == kModeMinibatch) {
+    const int64_t tab = (int64_t)c->V * c->ld;
+    if ((rc = dev_reserve(c->stream, &c->snap0, &c->snap0_cap, tab))) return rc;
+    if ((rc = dev_reserve(c->stream, &c->snap1, &c->snap1_cap, tab))) return rc;
+    HIPCHK(hipMemcpyAsync(c->snap0, c->syn0, sizeof(float) * tab, hipMemcpyDeviceToDevice,
+                          c->stream));
+    HIPCHK(hipMemcpyAsync(c->snap1, c->syn1, sizeof(float) * tab, hipMemcpyDeviceToDevice,
+                          c->stream));
+    rd0 = c->snap0;
+    rd1 = c->snap1;
+  }
+  if ((rc = run_sgns(c, c->d_job_exoff, mode, flags & G2V_FLAG_TIMING, rd0, rd1))) return rc;
+  // host arrays were copied asynchronously from pageable memory: finish before returning
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return G2V_OK;
+}
+
+int g2v_sync(g2v_ctx* c) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  HIPCHK(hipStreamSynchronize(c->stream));
+  return G2V_OK;
+}
+
+int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(out != nullptr, G2V_EINVAL, "out is null");
+  HIPCHK(hipStreamSynchronize(c->stream));
+  unsigned long long cnt[4] = {0, 0, 0, 0};
+  HIPCHK(hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(c->d_counters, 0, sizeof cnt));
+  memset(out, 0, sizeof *out);
+  out->effective_words = (int64_t)cnt[0];
+  out->examples = (int64_t)cnt[1];
+  out->raw_words = (int64_t)cnt[2];
+  out->jobs = c->jobs;
+  out->launches = c->launches;
+  for (auto& p : c->t_sgns) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
+    out->sgns_kernel_ms += ms;
+  }
+  for (auto& p : c->t_samp) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
+    out->sample_kernel_ms += ms;
+  }
+  c->t_sgns.clear();
+  c->t_samp.clear();
+  c->ev_used = 0;
+  c->jobs = 0;
+  c->launches = 0;
+  return G2V_OK;
+}
+
+}  // extern "C"

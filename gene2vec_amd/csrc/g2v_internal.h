@@ -1,0 +1,93 @@
+// g2v_internal.h -- constants and kernel argument blocks shared by the
+// kernels (g2v_kernels.hip) and the C-ABI implementation (g2v_api.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace g2v {
+
+// gensim 3.4.0 constants ([ext] word2vec_inner.pyx, base_any2vec.py)
+constexpr int kMaxExp = 6;
+constexpr int kExpTableSize = 1000;
+constexpr int kLutScale = kExpTableSize / kMaxExp / 2;  // C integer division: 83
+constexpr int kBatchWords = 10000;                      // batch_words == MAX_SENTENCE_LEN
+constexpr uint64_t kLcgMask = 281474976710655ULL;       // 2**48 - 1
+
+// LCG jump tables: n = lo + 2048 * hi, n < 2**22 (draws per job stay far below:
+// <= 10000 downsampling draws + K * 20000 negative draws)
+constexpr int kJumpBits = 11;
+constexpr int kJumpTab = 1 << kJumpBits;
+constexpr uint32_t kMaxJump = 1u << (2 * kJumpBits);
+
+// cum_table bucket index: x in [0, 2**31) -> bucket x >> 15 (65536 buckets)
+constexpr int kBucketShift = 15;
+constexpr int kBuckets = 1 << (31 - kBucketShift);
+
+constexpr int kSampleThreads = 256;
+constexpr int kSgnsThreads = 256;
+constexpr int kChunk = 32;  // consecutive examples a wave trains per grid-stride step
+
+constexpr int kModeHogwild = 0;
+constexpr int kModeSequential = 1;
+constexpr int kModeMinibatch = 2;
+
+struct LcgJump {
+  const uint64_t* a_lo;
+  const uint64_t* c_lo;
+  const uint64_t* a_hi;
+  const uint64_t* c_hi;
+};
+
+struct SampleArgs {
+  const int32_t* tok;
+  const int64_t* sent_off;  // nullptr when sent_len > 0
+  int64_t sent_len;
+  const int64_t* job_sent;  // [n_jobs+1] (absolute sentence index)
+  const uint64_t* job_seed;
+  const float* job_alpha;
+  int64_t job0;             // first job of this segment
+  const uint32_t* sample_int;
+  int sample_on;
+  const uint32_t* cum;
+  const int32_t* bkt;
+  int32_t V;
+  LcgJump jump;
+  int K;
+  int rec_stride;           // int32 words per record
+  int32_t* job_nex;         // [seg jobs]
+  const int64_t* job_exoff; // [seg jobs + 1]
+  int32_t* rec;
+  unsigned long long* counters;  // [0] effective words, [1] examples, [2] raw words
+};
+
+struct SgnsArgs {
+  const int32_t* rec;       // [E][rec_stride]: center, input, alpha bits, negs[K]
+  int rec_stride;
+  const int64_t* n_examples;  // device scalar E
+  const float* rd0;         // syn0 rows read
+  const float* rd1;         // syn1neg rows read
+  float* wr0;               // syn0 rows written (== rd0 unless MINIBATCH)
+  float* wr1;
+  const float* lockf;       // [V]
+  int64_t ld;               // row stride (floats), multiple of 4
+  int nvec;                 // ceil(D / 4): active float4 columns
+  const float* exp_table;   // [1000]
+};
+
+hipError_t launch_job_sample(bool write, const SampleArgs& a, int64_t n_jobs, hipStream_t st);
+hipError_t launch_scan_jobs(const int32_t* nex, int64_t nj, int64_t* off,
+                            unsigned long long* examples_total, hipStream_t st);
+hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
+                                   const int32_t* negs, int64_t n, int K, float alpha,
+                                   int rec_stride, int32_t* rec, hipStream_t st);
+bool sgns_supported(int K, int nv);
+hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int grid, hipStream_t st);
+int sgns_blocks_per_cu(int K, int nv);
+hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
+                        double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
+                        hipStream_t st);
+
+// host side: LCG jump tables (g2v_host.cpp)
+void lcg_jump_tables(uint64_t* a_lo, uint64_t* c_lo, uint64_t* a_hi, uint64_t* c_hi);
+
+}  // namespace g2v

@@ -1,0 +1,617 @@
+// g2v_kernels.hip -- CDNA4 (gfx950) kernels of the Gene2vec SGNS hot path.
+//
+// Replaces gensim 3.4.0's Cython/C inner loop ([ext] word2vec_inner.pyx:
+// train_batch_sg + fast_sentence_sg_neg + init())
+// that src/gene2vec.py:70,87 drives.  Three kernels per segment of jobs:
+//
+//   k_job_sample<false>  one workgroup per gensim job: OOV skip + frequent-word
+//                        downsampling with the job's 48-bit LCG (jumped ahead,
+//                        not iterated), window-1 example count
+//   k_scan_jobs          exclusive scan of per-job example counts
+//   k_job_sample<true>   same pass again, now writing one record per directed
+//                        example {center, input, alpha, negs[K]} with the K
+//                        negatives drawn exactly as gensim draws them (LCG state
+//                        = jump(seed, draws_before), bisect over cum_table
+//                        accelerated by a 2^16-bucket index)
+//   k_sgns<K,NV,MODE>    the update: ONE WAVE PER DIRECTED EXAMPLE, lane l owns
+//                        float4 columns l (+64): 16-B row gathers from
+//                        syn0/syn1neg, K+1 dots in fp64 (dsdot) reduced across the
+//                        wave by a value-halving xor butterfly, LUT sigmoid from
+//                        LDS, gradient + work accumulation in registers, and
+//                        plain (Hogwild) float4 write-back of every touched row.
+//
+// Everything is memory-gather bound (0.68 flop/B): no MFMA by design.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "g2v_internal.h"
+
+namespace g2v {
+
+// ---------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t lcg_step(uint64_t s) {
+  return (s * 25214903917ULL + 11ULL) & kLcgMask;
+}
+
+// state after n LCG steps: two table lookups (n = lo + 2048*hi)
+__device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint32_t n, const LcgJump& j) {
+  const uint32_t lo = n & (kJumpTab - 1), hi = n >> kJumpBits;
+  s = (j.a_lo[lo] * s + j.c_lo[lo]) & kLcgMask;
+  s = (j.a_hi[hi] * s + j.c_hi[hi]) & kLcgMask;
+  return s;
+}
+
+// bisect_left(cum, x, 0, V) restricted to the bucket that holds x
+__device__ __forceinline__ int32_t bisect_bucket(const uint32_t* __restrict__ cum,
+                                                 const int32_t* __restrict__ bkt, int32_t V,
+                                                 uint32_t x) {
+  const uint32_t b = x >> kBucketShift;
+  int32_t lo = bkt[b], hi = bkt[b + 1];
+  if (hi > V - 1) hi = V - 1;
+  while (hi > lo) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (cum[mid] >= x) hi = mid;
+    else lo = mid + 1;
+  }
+  return lo;
+}
+
+// one gensim negative draw: t = bisect_left(cum, (nr>>16) % cum[-1]); nr advances
+__device__ __forceinline__ int32_t draw_negative(uint64_t& nr, const uint32_t* __restrict__ cum,
+                                                 const int32_t* __restrict__ bkt, int32_t V,
+                                                 uint32_t cum_last) {
+  const uint32_t x = ((uint32_t)(nr >> 16)) % cum_last;
+  nr = lcg_step(nr);
+  return bisect_bucket(cum, bkt, V, x);
+}
+
+template <int NT>
+__device__ __forceinline__ int block_excl_scan(int v, int* sh, int& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  int base = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < NT / 64; ++w) {
+    const int t = sh[w];
+    base += (w < wid) ? t : 0;
+    tot += t;
+  }
+  __syncthreads();
+  total = tot;
+  return base + x - v;
+}
+
+__device__ __forceinline__ int64_t sent_start(const SampleArgs& a, int64_t s) {
+  return a.sent_len > 0 ? s * a.sent_len : a.sent_off[s];
+}
+
+// ---------------------------------------------------------------------------
+// k_job_sample: one workgroup per job ([ext] train_batch_sg pre-pass)
+// ---------------------------------------------------------------------------
+template <bool WRITE>
+__global__ __launch_bounds__(kSampleThreads) void k_job_sample(SampleArgs a) {
+  __shared__ int32_t s_eff[kBatchWords];       // kept tokens, compacted
+  __shared__ uint16_t s_kc[kBatchWords + 1];   // kept-before count per raw position
+  __shared__ int s_scan[kSampleThreads / 64];
+
+  const int64_t j = blockIdx.x;                // job within segment
+  const int64_t jg = a.job0 + j;
+  const int64_t s0 = a.job_sent[jg], s1 = a.job_sent[jg + 1];
+  const int64_t tb = sent_start(a, s0);
+  const int n = (int)(sent_start(a, s1) - tb);  // <= kBatchWords (host-checked)
+  const uint64_t seed = a.job_seed[jg];
+
+  int inv_base = 0, keep_base = 0;
+  for (int t0 = 0; t0 < n; t0 += kSampleThreads) {
+    const int t = t0 + threadIdx.x;
+    const int32_t w = (t < n) ? a.tok[tb + t] : -1;
+    const int inv = (w >= 0);
+    int tot_inv;
+    const int p = inv_base + block_excl_scan<kSampleThreads>(inv, s_scan, tot_inv);
+    int keep = inv;
+    if (inv && a.sample_on) {
+      // gensim: drop iff sample_int < random_int32(&next_random); the p-th draw
+      const uint32_t r = (uint32_t)(lcg_jump(seed, (uint32_t)p, a.jump) >> 16);
+      keep = !(a.sample_int[w] < r);
+    }
+    int tot_keep;
+    const int c = keep_base + block_excl_scan<kSampleThreads>(keep, s_scan, tot_keep);
+    if (t < n) {
+      s_kc[t] = (uint16_t)c;
+      if (keep) s_eff[c] = w;
+    }
+    inv_base += tot_inv;
+    keep_base += tot_keep;
+  }
+  if (threadIdx.x == 0) s_kc[n] = (uint16_t)keep_base;
+  __syncthreads();
+
+  const uint32_t ndraw = a.sample_on ? (uint32_t)inv_base : 0u;
+  const int ns = (int)(s1 - s0);
+  const float alpha = WRITE ? a.job_alpha[jg] : 0.f;
+  const int64_t out_base = WRITE ? a.job_exoff[j] : 0;
+  const uint32_t cum_last = a.cum[a.V - 1];
+  int ex_base = 0;
+  for (int q0 = 0; q0 < ns; q0 += kSampleThreads) {
+    const int q = q0 + threadIdx.x;
+    int e0 = 0, e1 = 0;
+    if (q < ns) {
+      e0 = s_kc[sent_start(a, s0 + q) - tb];
+      e1 = s_kc[sent_start(a, s0 + q + 1) - tb];
+    }
+    const int L = e1 - e0;
+    const int nex = L >= 2 ? 2 * (L - 1) : 0;  // window 1: (i,i-1),(i,i+1) in range
+    int tot;
+    const int eb = ex_base + block_excl_scan<kSampleThreads>(nex, s_scan, tot);
+    if (WRITE && nex) {
+      int e = eb;
+      for (int i = e0; i < e1; ++i) {
+#pragma unroll
+        for (int dj = -1; dj <= 1; dj += 2) {
+          const int jj = i + dj;
+          if (jj < e0 || jj >= e1) continue;
+          int32_t* r = a.rec + (out_base + e) * a.rec_stride;
+          const int32_t center = s_eff[i];
+          r[0] = center;
+          r[1] = s_eff[jj];
+          r[2] = __float_as_int(alpha);
+          uint64_t nr = lcg_jump(seed, ndraw + (uint32_t)a.K * (uint32_t)e, a.jump);
+          for (int d = 0; d < a.K; ++d) {
+            const int32_t t = draw_negative(nr, a.cum, a.bkt, a.V, cum_last);
+            r[3 + d] = (t == center) ? -1 : t;
+          }
+          ++e;
+        }
+      }
+    }
+    ex_base += tot;
+  }
+  if (!WRITE && threadIdx.x == 0) {
+    a.job_nex[j] = ex_base;
+    atomicAdd(a.counters + 0, (unsigned long long)keep_base);  // effective words
+    atomicAdd(a.counters + 2, (unsigned long long)n);          // raw words
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_scan_jobs: exclusive scan of the per-job example counts (one workgroup)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_scan_jobs(const int32_t* __restrict__ nex, int64_t nj,
+                                                    int64_t* __restrict__ off,
+                                                    unsigned long long* examples_total) {
+  __shared__ int s[16];
+  int64_t carry = 0;
+  for (int64_t b = 0; b < nj; b += 1024) {
+    const int64_t i = b + threadIdx.x;
+    const int v = i < nj ? nex[i] : 0;
+    int tot;
+    const int ex = block_excl_scan<1024>(v, s, tot);
+    if (i < nj) off[i] = carry + ex;
+    carry += tot;
+  }
+  if (threadIdx.x == 0) {
+    off[nj] = carry;
+    atomicAdd(examples_total, (unsigned long long)carry);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_explicit_records: records from host-provided (center, input, negs)
+// ---------------------------------------------------------------------------
+__global__ void k_explicit_records(const int32_t* __restrict__ center,
+                                   const int32_t* __restrict__ input,
+                                   const int32_t* __restrict__ negs, int64_t n, int K, float alpha,
+                                   int rec_stride, int32_t* __restrict__ rec) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int32_t* r = rec + i * rec_stride;
+  r[0] = center[i];
+  r[1] = input[i];
+  r[2] = __float_as_int(alpha);
+  for (int d = 0; d < K; ++d) {
+    const int32_t t = negs[i * K + d];
+    r[3 + d] = (t == center[i]) ? -1 : t;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// wave reductions (64 lanes)
+// ---------------------------------------------------------------------------
+template <int N>
+struct Pow2 {
+  static constexpr int v = (N <= 1) ? 1 : 2 * Pow2<(N + 1) / 2>::v;
+};
+template <>
+struct Pow2<1> {
+  static constexpr int v = 1;
+};
+
+__device__ __forceinline__ double shfl_xor_d(double v, int m) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __shfl_xor((int)(b & 0xffffffffLL), m, 64);
+  const int hi = __shfl_xor((int)(b >> 32), m, 64);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+__device__ __forceinline__ double wave_allreduce_d(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_d(v, m);
+  return v;
+}
+
+// Sum NT per-lane values over the 64 lanes: value-halving xor butterfly (each
+// exchange step halves the values a lane carries), then a plain butterfly on
+// the last one; the NT totals end up wave-uniform.
+template <int NT>
+__device__ __forceinline__ void wave_reduce_multi(const double (&in)[NT], double (&out)[NT],
+                                                  int lane) {
+  constexpr int P = Pow2<NT>::v;
+  static_assert(P <= 64, "too many values");
+  double x[P];
+#pragma unroll
+  for (int i = 0; i < P; ++i) x[i] = (i < NT) ? in[i] : 0.0;
+  int m = 32;
+#pragma unroll
+  for (int h = P / 2; h >= 1; h >>= 1) {
+    const bool up = (lane & m) != 0;
+#pragma unroll
+    for (int i = 0; i < h; ++i) {
+      const double send = up ? x[i] : x[i + h];
+      const double keep = up ? x[i + h] : x[i];
+      x[i] = keep + shfl_xor_d(send, m);
+    }
+    m >>= 1;
+  }
+#pragma unroll
+  for (; m >= 1; m >>= 1) x[0] += shfl_xor_d(x[0], m);
+  // value v lives in lanes whose halving bits spell v
+#pragma unroll
+  for (int v = 0; v < NT; ++v) {
+    int src = 0, mm = 32;
+#pragma unroll
+    for (int h = P / 2; h >= 1; h >>= 1) {
+      if (v & h) src += mm;
+      mm >>= 1;
+    }
+    out[v] = readlane_d(x[0], src);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_sgns: one wave per directed example ([ext] fast_sentence_sg_neg)
+// ---------------------------------------------------------------------------
+template <int K, int NV, int MODE>
+__global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
+  __shared__ float s_lut[kExpTableSize];
+  for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) s_lut[i] = a.exp_table[i];
+  __syncthreads();
+
+  constexpr int NT = K + 1;
+  const int lane = threadIdx.x & 63;
+  int64_t gw, nw;
+  if (MODE == kModeSequential) {
+    if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+    gw = 0;
+    nw = 1;
+  } else {
+    gw = (int64_t)blockIdx.x * (kSgnsThreads / 64) + (threadIdx.x >> 6);
+    nw = (int64_t)gridDim.x * (kSgnsThreads / 64);
+  }
+  const int64_t E = *a.n_examples;
+  const int64_t ld4 = a.ld >> 2;  // row stride in float4
+  bool on[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) on[v] = (lane + 64 * v) < a.nvec;
+
+  // no __restrict__: in HOGWILD/SEQUENTIAL mode rd* and wr* are the same tables
+  // and a wave's next example must see its own previous stores.
+  const float4* rd0 = reinterpret_cast<const float4*>(a.rd0);
+  const float4* rd1 = reinterpret_cast<const float4*>(a.rd1);
+  float4* wr0 = reinterpret_cast<float4*>(a.wr0);
+  float4* wr1 = reinterpret_cast<float4*>(a.wr1);
+
+  for (int64_t c = gw; c * kChunk < E; c += nw) {
+    const int64_t e_end = (c * kChunk + kChunk < E) ? c * kChunk + kChunk : E;
+    for (int64_t e = c * kChunk; e < e_end; ++e) {
+      const int32_t* __restrict__ r = a.rec + e * a.rec_stride;
+      int32_t tg[NT];
+      tg[0] = r[0];
+      const int32_t input = r[1];
+      const float alpha = __int_as_float(r[2]);
+#pragma unroll
+      for (int d = 0; d < K; ++d) tg[d + 1] = r[3 + d];
+
+      // gather: syn0[input] (frozen for the example) and the K+1 syn1neg rows
+      float4 l1[NV], rw[NT][NV];
+      const int64_t in_base = (int64_t)input * ld4 + lane;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        l1[v] = on[v] ? rd0[in_base + 64 * v] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        const int64_t tb = (int64_t)(tg[d] < 0 ? 0 : tg[d]) * ld4 + lane;
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+          rw[d][v] = (on[v] && tg[d] >= 0) ? rd1[tb + 64 * v] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+
+      // K+1 dots, products exact in fp64, summed in fp64 (dsdot semantics)
+      double pd[NT], dot[NT];
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        double s = 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          s = fma((double)l1[v].x, (double)rw[d][v].x, s);
+          s = fma((double)l1[v].y, (double)rw[d][v].y, s);
+          s = fma((double)l1[v].z, (double)rw[d][v].z, s);
+          s = fma((double)l1[v].w, (double)rw[d][v].w, s);
+        }
+        pd[d] = s;
+      }
+      wave_reduce_multi<NT>(pd, dot, lane);
+
+      float4 work[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) work[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      bool dirty[NT];
+      bool any = false;
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        dirty[d] = false;
+        if (tg[d] < 0) continue;
+        double dt = dot[d];
+        // a repeated target sees its own earlier update (gensim order)
+        bool prev_dirty = false;
+#pragma unroll
+        for (int d2 = 0; d2 < d; ++d2) {
+          if (tg[d2] == tg[d]) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) rw[d][v] = rw[d2][v];
+            prev_dirty = dirty[d2];
+          }
+        }
+        if (prev_dirty) {
+          double s = 0.0;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            s = fma((double)l1[v].x, (double)rw[d][v].x, s);
+            s = fma((double)l1[v].y, (double)rw[d][v].y, s);
+            s = fma((double)l1[v].z, (double)rw[d][v].z, s);
+            s = fma((double)l1[v].w, (double)rw[d][v].w, s);
+          }
+          dt = wave_allreduce_d(s);
+          dirty[d] = true;
+        }
+        const float f = (float)dt;
+        if (f <= -(float)kMaxExp || f >= (float)kMaxExp) continue;
+        const int idx = (int)((f + (float)kMaxExp) * (float)kLutScale);
+        const float g = ((d == 0 ? 1.0f : 0.0f) - s_lut[idx]) * alpha;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          work[v].x = __fmaf_rn(g, rw[d][v].x, work[v].x);
+          work[v].y = __fmaf_rn(g, rw[d][v].y, work[v].y);
+          work[v].z = __fmaf_rn(g, rw[d][v].z, work[v].z);
+          work[v].w = __fmaf_rn(g, rw[d][v].w, work[v].w);
+          rw[d][v].x = __fmaf_rn(g, l1[v].x, rw[d][v].x);
+          rw[d][v].y = __fmaf_rn(g, l1[v].y, rw[d][v].y);
+          rw[d][v].z = __fmaf_rn(g, l1[v].z, rw[d][v].z);
+          rw[d][v].w = __fmaf_rn(g, l1[v].w, rw[d][v].w);
+        }
+        dirty[d] = true;
+        any = true;
+      }
+
+      // write-back: each touched syn1neg row once (its last occurrence)
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        bool later = false;
+#pragma unroll
+        for (int d2 = d + 1; d2 < NT; ++d2) later |= (tg[d2] == tg[d]);
+        if (!dirty[d] || later) continue;
+        const int64_t tb = (int64_t)tg[d] * ld4 + lane;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          if (!on[v]) continue;
+          if (MODE == kModeMinibatch) {
+            const float4 o = rd1[tb + 64 * v];
+            float* p = reinterpret_cast<float*>(&wr1[tb + 64 * v]);
+            atomicAdd(p + 0, rw[d][v].x - o.x);
+            atomicAdd(p + 1, rw[d][v].y - o.y);
+            atomicAdd(p + 2, rw[d][v].z - o.z);
+            atomicAdd(p + 3, rw[d][v].w - o.w);
+          } else {
+            wr1[tb + 64 * v] = rw[d][v];
+          }
+        }
+      }
+      if (any) {
+        const float lf = a.lockf[input];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          if (!on[v]) continue;
+          float4 o;
+          o.x = __fmaf_rn(lf, work[v].x, l1[v].x);
+          o.y = __fmaf_rn(lf, work[v].y, l1[v].y);
+          o.z = __fmaf_rn(lf, work[v].z, l1[v].z);
+          o.w = __fmaf_rn(lf, work[v].w, l1[v].w);
+          if (MODE == kModeMinibatch) {
+            float* p = reinterpret_cast<float*>(&wr0[in_base + 64 * v]);
+            atomicAdd(p + 0, o.x - l1[v].x);
+            atomicAdd(p + 1, o.y - l1[v].y);
+            atomicAdd(p + 2, o.z - l1[v].z);
+            atomicAdd(p + 3, o.w - l1[v].w);
+          } else {
+            wr0[in_base + 64 * v] = o;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// vocabulary tables on the device ([ext] prepare_vocab / make_cum_table)
+// ---------------------------------------------------------------------------
+// pow / sample_int in parallel; the two double sums stay sequential (one
+// thread) so the rounding sequence is gensim's.
+__global__ void k_vocab_pow(const int64_t* __restrict__ counts, int32_t V, double power,
+                            double* __restrict__ cpow) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < V) cpow[i] = pow((double)counts[i], power);
+}
+
+__global__ void k_vocab_seq(const int64_t* __restrict__ counts, const double* __restrict__ cpow,
+                            int32_t V, double sample, uint32_t* __restrict__ cum,
+                            uint32_t* __restrict__ sample_int) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  double z = 0.0;
+  int64_t total = 0;
+  for (int32_t i = 0; i < V; ++i) {
+    z += cpow[i];
+    total += counts[i];
+  }
+  double acc = 0.0;
+  for (int32_t i = 0; i < V; ++i) {
+    acc += cpow[i];
+    cum[i] = (uint32_t)rint(acc / z * 2147483647.0);
+  }
+  double thr;
+  if (sample == 0.0) thr = (double)total;
+  else if (sample < 1.0) thr = sample * (double)total;
+  else thr = (double)(int64_t)(sample * (3.0 + sqrt(5.0)) / 2.0);
+  for (int32_t i = 0; i < V; ++i) {
+    const double v = (double)counts[i];
+    double p = (sqrt(v / thr) + 1.0) * (thr / v);
+    if (p >= 1.0) p = 1.0;
+    const double si = rint(p * 4294967296.0);
+    sample_int[i] = si >= 4294967295.0 ? 0xffffffffu : (uint32_t)si;  // 2**32 == keep always
+  }
+}
+
+// bkt[b] = bisect_left(cum, b << kBucketShift), b in [0, kBuckets]
+__global__ void k_buckets(const uint32_t* __restrict__ cum, int32_t V, int32_t* __restrict__ bkt) {
+  const int32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b > kBuckets) return;
+  const uint64_t x = (uint64_t)b << kBucketShift;
+  int32_t lo = 0, hi = V;
+  while (hi > lo) {
+    const int32_t mid = (lo + hi) >> 1;
+    if ((uint64_t)cum[mid] >= x) hi = mid;
+    else lo = mid + 1;
+  }
+  bkt[b] = lo;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_job_sample(bool write, const SampleArgs& a, int64_t n_jobs, hipStream_t st) {
+  if (n_jobs <= 0) return hipSuccess;
+  if (write)
+    hipLaunchKernelGGL(k_job_sample<true>, dim3((unsigned)n_jobs), dim3(kSampleThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL(k_job_sample<false>, dim3((unsigned)n_jobs), dim3(kSampleThreads), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_jobs(const int32_t* nex, int64_t nj, int64_t* off,
+                            unsigned long long* examples_total, hipStream_t st) {
+  hipLaunchKernelGGL(k_scan_jobs, dim3(1), dim3(1024), 0, st, nex, nj, off, examples_total);
+  return hipGetLastError();
+}
+
+hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
+                                   const int32_t* negs, int64_t n, int K, float alpha,
+                                   int rec_stride, int32_t* rec, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const unsigned blocks = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_explicit_records, dim3(blocks), dim3(256), 0, st, center, input, negs, n, K,
+                     alpha, rec_stride, rec);
+  return hipGetLastError();
+}
+
+template <int K, int NV>
+static hipError_t launch_sgns_kn(const SgnsArgs& a, int mode, int grid, hipStream_t st) {
+  switch (mode) {
+    case kModeSequential:
+      hipLaunchKernelGGL((k_sgns<K, NV, kModeSequential>), dim3(1), dim3(kSgnsThreads), 0, st, a);
+      break;
+    case kModeMinibatch:
+      hipLaunchKernelGGL((k_sgns<K, NV, kModeMinibatch>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+      break;
+    default:
+      hipLaunchKernelGGL((k_sgns<K, NV, kModeHogwild>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+  }
+  return hipGetLastError();
+}
+
+template <int K>
+static hipError_t launch_sgns_k(const SgnsArgs& a, int nv, int mode, int grid, hipStream_t st) {
+  if (nv == 1) return launch_sgns_kn<K, 1>(a, mode, grid, st);
+  return launch_sgns_kn<K, 2>(a, mode, grid, st);
+}
+
+bool sgns_supported(int K, int nv) {
+  if (nv != 1 && nv != 2) return false;
+  switch (K) {
+    case 1: case 2: case 3: case 5: case 10: case 15: case 20: return true;
+    default: return false;
+  }
+}
+
+hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int grid, hipStream_t st) {
+  switch (K) {
+    case 1: return launch_sgns_k<1>(a, nv, mode, grid, st);
+    case 2: return launch_sgns_k<2>(a, nv, mode, grid, st);
+    case 3: return launch_sgns_k<3>(a, nv, mode, grid, st);
+    case 5: return launch_sgns_k<5>(a, nv, mode, grid, st);
+    case 10: return launch_sgns_k<10>(a, nv, mode, grid, st);
+    case 15: return launch_sgns_k<15>(a, nv, mode, grid, st);
+    case 20: return launch_sgns_k<20>(a, nv, mode, grid, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int sgns_blocks_per_cu(int K, int nv) {
+  int nb = 0;
+  hipError_t e = hipErrorInvalidValue;
+#define G2V_OCC(KK, NN)                                                                  \
+  if (K == KK && nv == NN)                                                               \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sgns<KK, NN, kModeHogwild>, \
+                                                     kSgnsThreads, 0);
+  G2V_OCC(1, 1) G2V_OCC(2, 1) G2V_OCC(3, 1) G2V_OCC(5, 1) G2V_OCC(10, 1) G2V_OCC(15, 1)
+  G2V_OCC(20, 1) G2V_OCC(1, 2) G2V_OCC(2, 2) G2V_OCC(3, 2) G2V_OCC(5, 2) G2V_OCC(10, 2)
+  G2V_OCC(15, 2) G2V_OCC(20, 2)
+#undef G2V_OCC
+  if (e != hipSuccess || nb <= 0) nb = 1;
+  return nb;
+}
+
+hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
+                        double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
+                        hipStream_t st) {
+  hipLaunchKernelGGL(k_vocab_pow, dim3((V + 255) / 256), dim3(256), 0, st, counts, V, power, cpow);
+  hipLaunchKernelGGL(k_vocab_seq, dim3(1), dim3(64), 0, st, counts, cpow, V, sample, cum,
+                     sample_int);
+  hipLaunchKernelGGL(k_buckets, dim3((kBuckets + 1 + 255) / 256), dim3(256), 0, st, cum, V, bkt);
+  return hipGetLastError();
+}
+
+}  // namespace g2v

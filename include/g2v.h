@@ -1,0 +1,174 @@
+/*
+ * g2v.h -- C ABI of libg2v.so, the MI355X-native Gene2vec SGNS engine.
+ *
+ * The reference's hot path is gensim 3.4.0's skip-gram negative-sampling
+ * trainer driven from src/gene2vec.py.  Its plug-in point is gensim's per-job
+ * hook [ext] Word2Vec._do_train_job(sentences, alpha, inits) ->
+ * word2vec_inner.train_batch_sg(model, sentences, alpha, work, compute_loss),
+ * called from BaseAny2VecModel._worker_loop threads; the whole hook sits behind
+ * the Python API used at src/gene2vec.py:70 (Word2Vec(...)), :86 (load) and
+ * :87 (model.train(...)).  gensim reaches it through Cython, not a C FFI; this
+ * header is the C ABI a ctypes binding (gene2vec_amd/_native.py) loads in its
+ * place.  Every entry point below cites the reference behaviour it replaces
+ * ([ext] = upstream gensim 3.4.0).
+ *
+ * Conventions
+ *   - C linkage, POD arguments only, no torch types.
+ *   - Every function returns int status: G2V_OK (0) or a negative G2V_E* code;
+ *     the message is in g2v_last_error() (thread-local).  Nothing aborts or
+ *     throws across the ABI.
+ *   - Host pointers are borrowed for the duration of the call only.  Device
+ *     pointers passed to g2v_bind_tables / g2v_set_corpus(G2V_CORPUS_DEVICE)
+ *     are borrowed until replaced or until g2v_destroy.
+ *   - All device work is enqueued on the context's HIP stream and is
+ *     asynchronous unless a function says it synchronises.
+ *   - Tables live on the device as [V][ld] fp32 rows, ld = row stride in
+ *     floats (a multiple of 32, i.e. 128-B aligned rows); the pad columns are
+ *     kept at zero.  Host-side tables are dense [V][D] row-major fp32.
+ */
+#ifndef G2V_H
+#define G2V_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define G2V_ABI_VERSION 1
+
+/* status codes */
+#define G2V_OK 0
+#define G2V_EINVAL (-1)     /* bad argument / unsupported configuration */
+#define G2V_EHIP (-2)       /* HIP runtime error */
+#define G2V_ENOMEM (-3)     /* allocation failed */
+#define G2V_ESTATE (-4)     /* call order violated (e.g. train before vocab) */
+#define G2V_ERANGE (-5)     /* input exceeds a documented limit */
+
+/* g2v_train / g2v_sgns_step_explicit modes */
+#define G2V_MODE_HOGWILD 0    /* production: many waves, lock-free (gensim workers=N) */
+#define G2V_MODE_SEQUENTIAL 1 /* one wave, examples in gensim order (workers=1) */
+#define G2V_MODE_MINIBATCH 2  /* step API only: all examples read the pre-step tables,
+                                 deltas summed (float atomics) */
+#define G2V_MODE_MASK 0x3u
+#define G2V_FLAG_TIMING 0x100u /* record HIP events around each SGNS kernel launch */
+
+/* g2v_set_corpus flags */
+#define G2V_CORPUS_DEVICE 0x1u /* tokens / sent_off are device pointers (borrowed) */
+
+/* limits */
+#define G2V_BATCH_WORDS 10000   /* gensim batch_words = MAX_SENTENCE_LEN */
+#define G2V_MAX_DIM 512
+#define G2V_EXP_TABLE_SIZE 1000
+
+typedef struct g2v_ctx g2v_ctx;
+
+typedef struct g2v_stats {
+    int64_t raw_words;        /* tokens in the trained sentences (gensim raw_word_count) */
+    int64_t effective_words;  /* tokens kept after OOV removal + downsampling (train_batch_sg's return) */
+    int64_t examples;         /* directed (center, context) SGNS examples trained */
+    int64_t jobs;             /* gensim jobs (<= 10000 raw words each) */
+    int64_t launches;         /* SGNS-kernel launches */
+    double sgns_kernel_ms;    /* sum of SGNS-kernel durations (G2V_FLAG_TIMING), else 0 */
+    double sample_kernel_ms;  /* sum of sampling-kernel durations (G2V_FLAG_TIMING), else 0 */
+} g2v_stats;
+
+/* ---- errors / version --------------------------------------------------- */
+const char *g2v_last_error(void);
+int g2v_abi_version(void);
+
+/* ---- context ------------------------------------------------------------- */
+/* Replaces gensim's Word2Vec(size=vector_size, window, negative, hs=0, sg=1)
+ * model state ([ext] BaseWordEmbeddingsModel.__init__; src/gene2vec.py:70).
+ * window must be 1 (src/gene2vec.py:62); negative in the compiled set
+ * {1,2,3,5,10,15,20}; 1 <= vector_size <= G2V_MAX_DIM. */
+int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t negative,
+               int32_t window, g2v_ctx **out);
+int g2v_destroy(g2v_ctx *ctx);
+/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
+/* Row stride (floats) the device tables use. */
+int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);
+
+/* ---- vocabulary -> sampling tables -------------------------------------- */
+/* Replaces [ext] Word2VecVocab.prepare_vocab (sample_int, A.2) and
+ * make_cum_table(power=ns_exponent, domain=2**31-1) (A.3).  counts are in
+ * index order (sorted by descending count).  Both tables are built ON THE
+ * DEVICE (sequential double accumulation, round-half-even) and are
+ * bit-identical to gensim's; optional host copies are returned (synchronises
+ * when either out pointer is non-NULL).  sample == 0 disables downsampling. */
+int g2v_set_vocab(g2v_ctx *ctx, const int64_t *counts, double sample, double ns_exponent,
+                  uint32_t *cum_out, uint32_t *sample_int_out);
+
+/* ---- weights --------------------------------------------------------------- */
+/* Borrow device tables (e.g. torch-owned, so torch.distributed can all-reduce
+ * them): syn0 = [ext] wv.vectors, syn1neg = [ext] trainables.syn1neg, both
+ * [V][ld] fp32, ld >= g2v_row_stride and a multiple of 4.  NULL, NULL returns
+ * to context-owned tables. */
+int g2v_bind_tables(g2v_ctx *ctx, float *syn0_dev, float *syn1neg_dev, int64_t ld);
+/* Upload host [V][D] tables (+ optional vectors_lockf[V], NULL = ones).
+ * Replaces the model-owned numpy arrays of [ext] reset_weights (A.4). */
+int g2v_set_weights(g2v_ctx *ctx, const float *syn0, const float *syn1neg, const float *lockf);
+/* Download to host [V][D]; either pointer may be NULL.  Synchronises. */
+int g2v_get_weights(g2v_ctx *ctx, float *syn0, float *syn1neg);
+
+/* ---- corpus ----------------------------------------------------------------- */
+/* Sentences as CSR: tokens[n_tokens] int32 vocabulary indices (-1 = out of
+ * vocabulary, skipped without drawing, as gensim's vlookup miss), sent_off[n_sent+1]
+ * int64.  sent_off may be NULL when every sentence has length sent_len > 0
+ * (gene pairs: sent_len = 2).  Replaces the list[list[str]] gensim receives at
+ * src/gene2vec.py:70,87.  Without G2V_CORPUS_DEVICE the arrays are copied. */
+int g2v_set_corpus(g2v_ctx *ctx, const int32_t *tokens, int64_t n_tokens, const int64_t *sent_off,
+                   int64_t n_sent, int64_t sent_len, uint32_t flags);
+
+/* ---- training ---------------------------------------------------------------- */
+/* Greedy job packing of [ext] BaseAny2VecModel._job_producer: a sentence joins
+ * the current job while raw words <= batch_words.  Writes job_sent[n_jobs+1]
+ * (sentence index boundaries) when job_sent != NULL and cap >= n_jobs+1.
+ * Host-only, no context.  Sentences longer than batch_words -> G2V_ERANGE. */
+int g2v_plan_jobs(const int64_t *sent_off, int64_t n_sent, int64_t sent_len, int64_t batch_words,
+                  int64_t *job_sent, int64_t cap, int64_t *n_jobs_out);
+
+/* Train jobs [0, n_jobs) over the current corpus: the replacement of the
+ * per-job hook train_batch_sg -> fast_sentence_sg_neg (A.5) for every job of a
+ * train() epoch.  job_sent[n_jobs+1] sentence boundaries (g2v_plan_jobs),
+ * job_alpha[n_jobs] the per-job learning rate of [ext] _update_job_params (A.6),
+ * job_seed[n_jobs] the per-job next_random = 2**24*randint(2**24)+randint(2**24)
+ * drawn from model.random.  Downsampling, the 48-bit LCG, the cum_table bisect and
+ * the window-1 example order reproduce gensim exactly; mode selects the
+ * update order (G2V_MODE_HOGWILD | G2V_MODE_SEQUENTIAL) | G2V_FLAG_TIMING. */
+int g2v_train(g2v_ctx *ctx, const int64_t *job_sent, const float *job_alpha,
+              const uint64_t *job_seed, int64_t n_jobs, uint32_t flags);
+
+/* Deterministic step with explicit negatives: n examples (center[i] = gensim
+ * word_index, input[i] = word2_index whose syn0 row is trained, negs[i*K..] with
+ * -1 = skipped), one learning rate.  Modes SEQUENTIAL / HOGWILD / MINIBATCH. */
+int g2v_sgns_step_explicit(g2v_ctx *ctx, const int32_t *center, const int32_t *input,
+                           const int32_t *negs, int64_t n, float alpha, uint32_t flags);
+
+/* Debug/parity: the (center, input, negs[K]) records the device sampler
+ * produces for jobs [0, n_jobs) (same arguments as g2v_train), written to
+ * rec_out[cap][K+2] in gensim order; *n_out = record count.  Synchronises. */
+int g2v_debug_sample(g2v_ctx *ctx, const int64_t *job_sent, const uint64_t *job_seed,
+                     int64_t n_jobs, int32_t *rec_out, int64_t cap, int64_t *n_out);
+
+/* ---- sync / stats ------------------------------------------------------------ */
+int g2v_sync(g2v_ctx *ctx);
+/* Accumulated since the previous call (synchronises, then resets). */
+int g2v_read_stats(g2v_ctx *ctx, g2v_stats *out);
+
+/* ---- host-native helpers (no device work) -------------------------------------- */
+/* [ext] Word2VecTrainables.seeded_vector for every row: row i =
+ * (RandomState(seeds[i]).rand(D) - 0.5) / D as float32, seeds[i] =
+ * hash(word_i + str(seed)) & 0xffffffff computed by the caller.  MT19937
+ * init_genrand + 53-bit random_sample, bit-identical to numpy's RandomState. */
+int g2v_seeded_vectors(const uint32_t *seeds, int64_t n_rows, int32_t dim, float *out);
+/* counts[V] and first-occurrence position first[V] (-1 = absent) of int ids in
+ * [0, V) over ids[n]; the vocabulary scan of [ext] scan_vocab on pre-hashed ids. */
+int g2v_count_ids(const int32_t *ids, int64_t n, int32_t V, int64_t *counts, int64_t *first);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* G2V_H */

@@ -1,0 +1,90 @@
+"""libg2v.so loads here (no GPU), exports every symbol include/g2v.h
+declares, and its host-only helpers match the oracle / numpy."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from gene2vec_amd import _native as N
+from gene2vec_amd import engine as E
+from oracle import sgns_oracle as O
+from tests.conftest import ROOT
+from tests.helpers import crc_hash
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "g2v.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(g2v_[a-z_0-9]+)\s*\(", src)))
+
+
+def test_library_loads_and_exports_header():
+    L = N.lib()
+    syms = header_symbols()
+    assert len(syms) >= 18
+    for s in syms:
+        assert hasattr(L, s), s
+        assert s in N.SIGNATURES, f"{s} missing from the ctypes signature table"
+    assert set(N.SIGNATURES) == set(syms)
+    assert L.g2v_abi_version() == 1
+
+
+def test_error_path_without_gpu_is_loud():
+    # creating a context needs a device; on a CPU box it must fail with a
+    # status code and a message, never crash
+    import ctypes as C
+    h = C.c_void_p()
+    rc = N.lib().g2v_create(0, 10, 8, 5, 2, C.byref(h))  # window=2 rejected up front
+    assert rc == N.G2V_EINVAL
+    assert b"window" in N.lib().g2v_last_error()
+    rc = N.lib().g2v_create(0, 10, 8, 4, 1, C.byref(h))  # negative=4 not compiled
+    assert rc == N.G2V_EINVAL
+
+
+@pytest.mark.parametrize("lengths", [[2] * 40, [2] * 12345, [2, 4, 0, 2, 3, 9997, 2, 10000, 1] * 3,
+                                     [], [0, 0, 0], [10000, 10000], [5000, 5000, 1]])
+def test_plan_jobs_matches_oracle(lengths):
+    ref = O.plan_jobs(lengths)
+    off = np.cumsum([0] + lengths).astype(np.int64)
+    js = E.plan_jobs(sent_off=off)
+    expect = [ref[0][0]] + [j[1] for j in ref] if ref else [0]
+    assert js.tolist() == expect
+
+
+def test_plan_jobs_uniform_and_limits():
+    js = E.plan_jobs(n_sent=12345, sent_len=2)
+    assert js.tolist() == [j[0] for j in O.plan_jobs([2] * 12345)] + [12345]
+    with pytest.raises(N.G2VError):
+        E.plan_jobs(sent_off=np.array([0, 10001], np.int64))
+
+
+def test_job_alphas_and_seeds(golden):
+    s = golden["schedule"]
+    js = E.plan_jobs(n_sent=1000000, sent_len=2)
+    a = E.job_alphas(js, 1000000)
+    assert a[:5].tolist() == s["alphas1m_head"] and a[-5:].tolist() == s["alphas1m_tail"]
+    js40 = E.plan_jobs(n_sent=40, sent_len=2)
+    assert E.job_alphas(js40, 40, cur_epoch=1, epochs=3).tolist() == s["epoch2of3"]
+    assert E.job_seeds(np.random.RandomState(1), 5).tolist() == s["seeds_rs1"]
+    # vectorised == the oracle's per-job Python loop on an irregular corpus
+    lengths = list(np.random.RandomState(3).randint(0, 7, 30000))
+    jobs = O.plan_jobs(lengths)
+    js = E.plan_jobs(sent_off=np.cumsum([0] + lengths))
+    assert E.job_alphas(js, len(lengths)).tolist() == O.job_alphas(jobs, len(lengths))
+
+
+def test_seeded_vectors_native_is_numpy_randomstate():
+    words = ["TLE1", "ALDOB", "G00017", "x" * 40]
+    seeds = np.array([crc_hash(w + "1") & 0xFFFFFFFF for w in words], np.uint32)
+    for dim in (1, 7, 200, 512):
+        got = E.seeded_vectors(seeds, dim)
+        for i, w in enumerate(words):
+            ref = O.seeded_vector(w + "1", dim, crc_hash).astype(np.float32)
+            assert np.array_equal(got[i], ref)
+
+
+def test_count_ids():
+    ids = np.array([3, 1, 3, 0, 3, 1], np.int32)
+    c, f = E.count_ids(ids, 5)
+    assert c.tolist() == [1, 2, 0, 3, 0] and f.tolist() == [3, 1, -1, 0, -1]

@@ -1,0 +1,153 @@
+"""The CPU oracle against the golden fixtures and the independent anchors.
+
+Anchors independent of the oracle itself: the reference's own corpus
+data/test.txt (counts / vocabulary size, SURVEY.md section 4 KATs) and numpy's
+RandomState (the generator gensim calls in seeded_vector / model.random).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import c_oracle as CO
+from oracle import sgns_oracle as O
+from tests.conftest import GOLDEN
+from tests.helpers import crc_hash
+
+
+def test_reference_fixture_vocab(golden, test_pairs):
+    voc = O.build_vocab(test_pairs, 1, 1e-3)
+    # 80 raw words, 79 unique, TLE1 x2 at index 0
+    assert voc.total_words == 80 and len(voc.index2word) == 79 and voc.corpus_count == 40
+    assert voc.index2word[0] == "TLE1" and voc.counts[0] == 2
+    g = golden["test_pairs"]
+    assert voc.index2word == g["index2word"]
+    assert voc.first_order == g["first_order"]
+    assert voc.counts.tolist() == g["counts"]
+
+
+def test_known_answer_tables(golden):
+    g = golden["test_pairs"]
+    cum = g["cum_table"]
+    assert cum[:4] == [45325569, 72276314, 99227058, 126177803]
+    assert cum[-1] == 2 ** 31 - 1
+    si = dict(zip(g["counts"], g["sample_int"]))
+    assert si[1] == 1558397584 and si[2] == 1030792151
+    assert set(g["sample_int_s0"]) == {2 ** 32}  # sample=0: never downsampled
+
+
+def test_oracle_tables_match_golden(golden, test_pairs):
+    voc = O.build_vocab(test_pairs, 1, 1e-3)
+    assert O.make_cum_table(voc.counts).tolist() == golden["test_pairs"]["cum_table"]
+    assert [int(x) for x in voc.sample_int] == golden["test_pairs"]["sample_int"]
+    for V in (1000, 24447, 60000):
+        z = np.load(os.path.join(GOLDEN, f"zipf{V}_tables.npz"))
+        assert np.array_equal(CO.make_cum_table(z["counts"]), z["cum"])
+        assert np.array_equal(CO.sample_int(z["counts"], 1e-3), z["sample_int"])
+    z = np.load(os.path.join(GOLDEN, "zipf1000_tables.npz"))
+    assert np.array_equal(O.make_cum_table(z["counts"]), z["cum"])
+
+
+def test_exp_table():
+    g = np.load(os.path.join(GOLDEN, "exp_table.npy"))
+    assert np.array_equal(O.exp_table(), g)
+    assert np.array_equal(CO.exp_table(), g)
+    assert O.LUT_SCALE == 83
+    # monotone sigmoid over [-6, 6)
+    assert np.all(np.diff(g) > 0) and 0 < g[0] < 0.003 and 0.997 < g[-1] < 1
+
+
+def test_lcg_and_negatives(golden):
+    g = golden["lcg"]
+    z = np.load(os.path.join(GOLDEN, "zipf1000_tables.npz"))
+    x = g["seed"]
+    outs, negs = [], []
+    for _ in range(1000):
+        outs.append(x >> 16)
+        t, x = O.draw_negative(z["cum"], x)
+        negs.append(t)
+    assert outs == g["outputs"] and negs == g["negatives_zipf1000"]
+    y = g["seed"]
+    for _ in range(1000):
+        y = O.lcg_next(y)
+    assert y == O.lcg_jump(g["seed"], 1000) == g["jump_1000"]
+    assert O.lcg_jump(g["seed"], 123457) == g["jump_123457"]
+
+
+def test_schedule(golden):
+    s = golden["schedule"]
+    assert [list(j) for j in O.plan_jobs([2] * 40)] == s["jobs40"]
+    assert O.job_alphas(O.plan_jobs([2] * 40), 40) == s["alphas40"] == [0.025]
+    j = O.plan_jobs([2] * 1000000)
+    assert len(j) == s["jobs1m_n"] == 200
+    a = O.job_alphas(j, 1000000)
+    assert a[:5] == s["alphas1m_head"] and a[-5:] == s["alphas1m_tail"]
+    assert a[1] == pytest.approx(0.025 - 0.0249 * 5000 / 1e6, rel=1e-15)
+    assert [list(x) for x in O.plan_jobs(s["mixed_lengths"])] == s["mixed_jobs"]
+    assert O.job_seeds(np.random.RandomState(1), 5) == s["seeds_rs1"]
+
+
+def test_seeded_vector_is_numpy_randomstate(golden):
+    g = golden["seeded_vector"]
+    v = O.seeded_vector(g["word"] + str(g["seed"]), g["dim"], crc_hash).astype(np.float32)
+    assert v.tolist() == g["values"]
+    rs = np.random.RandomState(crc_hash("TLE11") & 0xFFFFFFFF)
+    assert np.array_equal(((rs.rand(8) - 0.5) / 8).astype(np.float32), v)
+
+
+@pytest.mark.parametrize("name", ["step_V60_D200_K5", "step_V40_D512_K15"])
+def test_step_golden_numpy_and_c(name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    for impl in ("numpy", "c"):
+        a0, a1 = z["syn0"].copy(), z["syn1neg"].copy()
+        lockf = np.ones(len(a0), dtype=np.float32)
+        if impl == "numpy":
+            O.sgns_step_sequential(a0, a1, lockf, z["center"], z["input"], z["negs"],
+                                   float(z["alpha"]))
+        else:
+            CO.sgns_step_sequential(a0, a1, lockf, z["center"], z["input"], z["negs"],
+                                    float(z["alpha"]))
+        np.testing.assert_allclose(a0, z["syn0_out"], rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(a1, z["syn1neg_out"], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("tag,sample", [("s0", 0.0), ("s1e-3", 1e-3)])
+def test_e2e_numpy_vs_c_vs_golden(test_pairs, tag, sample):
+    z = np.load(os.path.join(GOLDEN, f"e2e_test_pairs_{tag}.npz"))
+    voc = O.build_vocab(test_pairs, 1, sample)
+    syn0, syn1, lockf = O.reset_weights(voc.index2word, 200, 1, crc_hash)
+    assert np.array_equal(syn0, z["syn0_init"])
+    ids = O.sentences_to_ids(test_pairs, voc.word2index)
+    tok = np.array([w for s in ids for w in s], np.int32)
+    off = np.cumsum([0] + [len(s) for s in ids]).astype(np.int64)
+    jobs = O.plan_jobs([len(s) for s in ids])
+    js = np.array([jobs[0][0]] + [j[1] for j in jobs], np.int64)
+    cum = O.make_cum_table(voc.counts)
+    rs = np.random.RandomState(1)
+    stats = []
+    for _ in range(3):
+        al = np.array(O.job_alphas(jobs, len(ids)), np.float32)
+        sd = np.array(O.job_seeds(rs, len(jobs)), np.uint64)
+        stats.append(CO.train(tok, off, js, al, sd, voc.sample_int, bool(sample), cum, syn0,
+                              syn1, lockf, 5))
+    gst = json.loads(str(z["stats"]))
+    for a, b in zip(stats, gst):
+        assert (a["effective_words"], a["examples"], a["jobs"]) == (
+            b["effective_words"], b["examples"], b["jobs"])
+    np.testing.assert_allclose(syn0, z["syn0"], rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(syn1, z["syn1neg"], rtol=1e-6, atol=1e-8)
+    assert np.abs(syn1).max() > 0  # it trained
+
+
+def test_c_records_match_numpy(test_pairs):
+    voc = O.build_vocab(test_pairs, 1, 1e-3)
+    ids = O.sentences_to_ids(test_pairs, voc.word2index)
+    cum = O.make_cum_table(voc.counts)
+    tok = np.array([w for s in ids for w in s], np.int32)
+    off = np.cumsum([0] + [len(s) for s in ids]).astype(np.int64)
+    for seed in (1, 987654321, 2 ** 47 + 5):
+        rec = CO.sample_records(tok, off, np.array([0, len(ids)]), np.array([seed], np.uint64),
+                                voc.sample_int, True, cum, 5)
+        ref = O.sample_job_records(ids, seed, voc.sample_int, True, cum, 5)
+        assert rec.tolist() == [[c, j] + n for c, j, n in ref]
