@@ -24,6 +24,11 @@ MODE_SEQUENTIAL = 1
 MODE_MINIBATCH = 2
 FLAG_TIMING = 0x100
 CORPUS_DEVICE = 0x1
+OPT_HOT_ROWS = 1
+OPT_CACHE_POLICY = 2
+OPT_SEG_JOBS = 3
+OPT_GRID = 4
+OPT_TABLE_MEM = 5
 BATCH_WORDS = 10000
 MAX_DIM = 512
 SUPPORTED_NEGATIVE = (1, 2, 3, 5, 10, 15, 20)
@@ -62,6 +67,7 @@ SIGNATURES = {
     "g2v_create": (C.c_int, [C.c_int, _i32, _i32, _i32, _i32, C.POINTER(_vp)]),
     "g2v_destroy": (C.c_int, [_vp]),
     "g2v_set_stream": (C.c_int, [_vp, _vp]),
+    "g2v_set_option": (C.c_int, [_vp, C.c_int, _i64]),
     "g2v_row_stride": (C.c_int, [_vp, C.POINTER(_i64)]),
     "g2v_set_vocab": (C.c_int, [_vp, _vp, _f64, _f64, _vp, _vp]),
     "g2v_bind_tables": (C.c_int, [_vp, _vp, _vp, _i64]),

@@ -91,6 +91,8 @@ struct g2v_ctx {
   int nv = 1, nvec = 0, rec_stride = 0;
   int64_t ld = 0;
   int cus = 0, sgns_grid = 0;
+  int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
+  int cache_policy = 1;         // kPolWt
   hipStream_t own_stream = nullptr, stream = nullptr;
 
   float *own0 = nullptr, *own1 = nullptr;  // context-owned tables
@@ -146,6 +148,13 @@ struct g2v_ctx {
   size_t ev_used = 0;
   std::vector<std::pair<hipEvent_t, hipEvent_t>> t_sgns, t_samp;
 };
+
+// Hogwild staleness bound: with more than ~2k waves in flight the summed
+// stale updates of the hottest rows destabilise SGD (measured at V=24447:
+// 512 workgroups track the sequential oracle, 1024 diverge in iteration 1).
+static int default_grid(int cus, int K, int nv) {
+  return std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
+}
 
 static int ctx_event(g2v_ctx* c, hipEvent_t* out) {
   if (c->ev_used == c->ev_pool.size()) {
@@ -210,7 +219,7 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
   if (hipGetDeviceProperties(&prop, device) != hipSuccess)
     return bail(fail(G2V_EHIP, "hipGetDeviceProperties failed"));
   c->cus = prop.multiProcessorCount;
-  c->sgns_grid = c->cus * sgns_blocks_per_cu(negative, nv);
+  c->sgns_grid = default_grid(c->cus, negative, nv);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(G2V_EHIP, "hipStreamCreate failed"));
   c->stream = c->own_stream;
@@ -218,6 +227,8 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
     return bail(fail(G2V_EHIP, "hipEventCreate failed"));
 
   const size_t tab = (size_t)c->V * (size_t)c->ld;
+  if (tab * sizeof(float) > 0x7fffffffull)
+    return bail(fail(G2V_ERANGE, "table of %zu bytes exceeds the 2 GiB buffer-offset range", tab * 4));
   if ((rc = dev_alloc(&c->own0, tab)) || (rc = dev_alloc(&c->own1, tab)) ||
       (rc = dev_alloc(&c->lockf, (size_t)c->V)) || (rc = dev_alloc(&c->exp_table, kExpTableSize)) ||
       (rc = dev_alloc(&c->jump, 4 * (size_t)kJumpTab)) || (rc = dev_alloc(&c->cum, (size_t)c->V)) ||
@@ -293,6 +304,54 @@ int g2v_set_stream(g2v_ctx* c, void* s) {
   if (rc) return rc;
   c->stream = s ? (hipStream_t)s : c->own_stream;
   return G2V_OK;
+}
+
+int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  switch (key) {
+    case G2V_OPT_HOT_ROWS:
+      REQUIRE(value >= -1 && value <= c->V, G2V_EINVAL, "hot_rows %lld out of [-1, V]",
+              (long long)value);
+      c->hot_rows = (int)value;
+      return G2V_OK;
+    case G2V_OPT_CACHE_POLICY:
+      REQUIRE(value >= 0 && value <= 2, G2V_EINVAL, "cache policy %lld out of [0, 2]",
+              (long long)value);
+      c->cache_policy = (int)value;
+      return G2V_OK;
+    case G2V_OPT_SEG_JOBS:
+      REQUIRE(value >= 1, G2V_EINVAL, "seg_jobs must be >= 1");
+      c->seg_jobs = value;
+      return G2V_OK;
+    case G2V_OPT_TABLE_MEM: {
+      // 0 hipMalloc (coarse-grained), 1 fine-grained, 2 uncached; contents reset to 0
+      REQUIRE(value >= 0 && value <= 2, G2V_EINVAL, "table mem kind %lld out of [0, 2]",
+              (long long)value);
+      HIPCHK(hipStreamSynchronize(c->stream));
+      const bool bound = c->syn0 != c->own0;
+      dev_free(c->own0);
+      dev_free(c->own1);
+      const size_t bytes = sizeof(float) * (size_t)c->V * (size_t)(((int64_t)c->D + 31) / 32 * 32);
+      const unsigned fl = value == 0 ? hipDeviceMallocDefault
+                          : value == 1 ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+      HIPCHK(hipExtMallocWithFlags((void**)&c->own0, bytes, fl));
+      HIPCHK(hipExtMallocWithFlags((void**)&c->own1, bytes, fl));
+      HIPCHK(hipMemset(c->own0, 0, bytes));
+      HIPCHK(hipMemset(c->own1, 0, bytes));
+      if (!bound) {
+        c->syn0 = c->own0;
+        c->syn1 = c->own1;
+      }
+      return G2V_OK;
+    }
+    case G2V_OPT_GRID:
+      REQUIRE(value >= 0, G2V_EINVAL, "grid must be >= 0");
+      c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv);
+      return G2V_OK;
+    default:
+      return fail(G2V_EINVAL, "unknown option key %d", key);
+  }
 }
 
 int g2v_row_stride(g2v_ctx* c, int64_t* ld_out) {
@@ -546,6 +605,9 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.lockf = c->lockf;
   s.ld = c->ld;
   s.nvec = c->nvec;
+  s.D = c->D;
+  s.V = c->V;
+  s.hot_rows = c->hot_rows < 0 ? c->V : std::min(c->hot_rows, c->V);
   s.exp_table = c->exp_table;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc;
@@ -553,7 +615,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
     HIPCHK(hipEventRecord(e0, c->stream));
   }
-  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->sgns_grid, c->stream));
+  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
   if (timing) {
     HIPCHK(hipEventRecord(e1, c->stream));
     c->t_sgns.emplace_back(e0, e1);

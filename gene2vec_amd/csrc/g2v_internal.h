@@ -71,6 +71,9 @@ struct SgnsArgs {
   const float* lockf;       // [V]
   int64_t ld;               // row stride (floats), multiple of 4
   int nvec;                 // ceil(D / 4): active float4 columns
+  int D;
+  int V;
+  int hot_rows;             // rows [0, hot_rows) are updated with float atomics
   const float* exp_table;   // [1000]
 };
 
@@ -81,7 +84,8 @@ hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
                                    const int32_t* negs, int64_t n, int K, float alpha,
                                    int rec_stride, int32_t* rec, hipStream_t st);
 bool sgns_supported(int K, int nv);
-hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int grid, hipStream_t st);
+hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int pol, int grid,
+                       hipStream_t st);
 int sgns_blocks_per_cu(int K, int nv);
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
                         double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,

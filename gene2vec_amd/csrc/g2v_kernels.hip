@@ -296,35 +296,103 @@ __device__ __forceinline__ void wave_reduce_multi(const double (&in)[NT], double
 // ---------------------------------------------------------------------------
 // k_sgns: one wave per directed example ([ext] fast_sentence_sg_neg)
 // ---------------------------------------------------------------------------
-template <int K, int NV, int MODE>
+// Table traffic goes through buffer resources so every load/store carries an
+// explicit cache policy (POL, compile time):
+//   kPolPlain   default policy (lines stay in the issuing XCD's L2)
+//   kPolWt      stores sc1 (write-through to the coherent side, line dropped
+//               from the writer's L2) -- other XCDs see updates within the launch
+//   kPolWtRd    kPolWt + sc1 loads
+// Rows with vocabulary index < hot_rows (the most frequent genes: indices are
+// sorted by descending count) are never stored: their deltas go to the memory
+// side as float atomics, one 256-B contiguous wave-instruction per 64 columns,
+// so concurrent updates of a hot row are summed, not lost.
+constexpr int kPolPlain = 0;
+constexpr int kPolWt = 1;
+constexpr int kPolWtRd = 2;
+
+template <int POL>
+struct Pol {
+  static constexpr int ld = (POL == kPolWtRd) ? 16 : 0;  // sc1
+  static constexpr int st = (POL == kPolPlain) ? 0 : 16;  // sc1
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0,
+                                           (int)(bytes > 0x7fffffff ? 0x7fffffff : bytes),
+                                           0x00020000);
+}
+
+template <int AUX>
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, int off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+  float4 o;
+  o.x = __uint_as_float(v[0]);
+  o.y = __uint_as_float(v[1]);
+  o.z = __uint_as_float(v[2]);
+  o.w = __uint_as_float(v[3]);
+  return o;
+}
+
+template <int AUX>
+__device__ __forceinline__ void bstore4(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+  u4 u;
+  u[0] = __float_as_uint(v.x);
+  u[1] = __float_as_uint(v.y);
+  u[2] = __float_as_uint(v.z);
+  u[3] = __float_as_uint(v.w);
+  __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, AUX);
+}
+
+template <int AUX>
+__device__ __forceinline__ float bload1(__amdgpu_buffer_rsrc_t r, int off) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, off, 0, AUX));
+}
+
+__device__ __forceinline__ double dot4(const float4& a, const float4& b, double s) {
+  s = fma((double)a.x, (double)b.x, s);
+  s = fma((double)a.y, (double)b.y, s);
+  s = fma((double)a.z, (double)b.z, s);
+  s = fma((double)a.w, (double)b.w, s);
+  return s;
+}
+
+template <int K, int NV, int MODE, int POL>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
   __shared__ float s_lut[kExpTableSize];
+  __shared__ float s_work[kSgnsThreads / 64][64 * 4 * NV];  // per-wave transpose buffer
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) s_lut[i] = a.exp_table[i];
   __syncthreads();
 
   constexpr int NT = K + 1;
+  constexpr int LA = Pol<POL>::ld, SA = Pol<POL>::st;
+  constexpr int NE = NV * 4;  // element-layout columns per lane (l + 64 i)
   const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
   int64_t gw, nw;
   if (MODE == kModeSequential) {
     if (blockIdx.x != 0 || threadIdx.x >= 64) return;
     gw = 0;
     nw = 1;
   } else {
-    gw = (int64_t)blockIdx.x * (kSgnsThreads / 64) + (threadIdx.x >> 6);
+    gw = (int64_t)blockIdx.x * (kSgnsThreads / 64) + wid;
     nw = (int64_t)gridDim.x * (kSgnsThreads / 64);
   }
   const int64_t E = *a.n_examples;
-  const int64_t ld4 = a.ld >> 2;  // row stride in float4
+  const int D = a.D;
+  const int64_t tbytes = (int64_t)a.V * a.ld * 4;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.rd0, tbytes);
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.rd1, tbytes);
+  const __amdgpu_buffer_rsrc_t w0 = make_rsrc(a.wr0, tbytes);
+  const __amdgpu_buffer_rsrc_t w1 = make_rsrc(a.wr1, tbytes);
+  const int hot = (MODE == kModeSequential || MODE == kModeMinibatch) ? 0 : a.hot_rows;
+  const int rowb = (int)a.ld * 4;  // row stride in bytes
   bool on[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) on[v] = (lane + 64 * v) < a.nvec;
-
-  // no __restrict__: in HOGWILD/SEQUENTIAL mode rd* and wr* are the same tables
-  // and a wave's next example must see its own previous stores.
-  const float4* rd0 = reinterpret_cast<const float4*>(a.rd0);
-  const float4* rd1 = reinterpret_cast<const float4*>(a.rd1);
-  float4* wr0 = reinterpret_cast<float4*>(a.wr0);
-  float4* wr1 = reinterpret_cast<float4*>(a.wr1);
+  bool eon[NE];
+#pragma unroll
+  for (int i = 0; i < NE; ++i) eon[i] = (lane + 64 * i) < D;
 
   for (int64_t c = gw; c * kChunk < E; c += nw) {
     const int64_t e_end = (c * kChunk + kChunk < E) ? c * kChunk + kChunk : E;
@@ -339,16 +407,27 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
 
       // gather: syn0[input] (frozen for the example) and the K+1 syn1neg rows
       float4 l1[NV], rw[NT][NV];
-      const int64_t in_base = (int64_t)input * ld4 + lane;
+      const int in_off = input * rowb + lane * 16;
 #pragma unroll
       for (int v = 0; v < NV; ++v)
-        l1[v] = on[v] ? rd0[in_base + 64 * v] : make_float4(0.f, 0.f, 0.f, 0.f);
+        l1[v] = on[v] ? bload4<LA>(r0, in_off + 1024 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
-        const int64_t tb = (int64_t)(tg[d] < 0 ? 0 : tg[d]) * ld4 + lane;
+        const int off = (tg[d] < 0 ? 0 : tg[d]) * rowb + lane * 16;
 #pragma unroll
         for (int v = 0; v < NV; ++v)
-          rw[d][v] = (on[v] && tg[d] >= 0) ? rd1[tb + 64 * v] : make_float4(0.f, 0.f, 0.f, 0.f);
+          rw[d][v] = (on[v] && tg[d] >= 0) ? bload4<LA>(r1, off + 1024 * v)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      bool any_hot = false;
+#pragma unroll
+      for (int d = 0; d < NT; ++d) any_hot |= (tg[d] >= 0 && tg[d] < hot);
+      // element layout of syn0[input] for coalesced atomics (hot targets only)
+      float l1e[NE];
+      if (any_hot) {
+#pragma unroll
+        for (int i = 0; i < NE; ++i)
+          l1e[i] = eon[i] ? bload1<LA>(r0, input * rowb + (lane + 64 * i) * 4) : 0.f;
       }
 
       // K+1 dots, products exact in fp64, summed in fp64 (dsdot semantics)
@@ -357,12 +436,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
       for (int d = 0; d < NT; ++d) {
         double s = 0.0;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          s = fma((double)l1[v].x, (double)rw[d][v].x, s);
-          s = fma((double)l1[v].y, (double)rw[d][v].y, s);
-          s = fma((double)l1[v].z, (double)rw[d][v].z, s);
-          s = fma((double)l1[v].w, (double)rw[d][v].w, s);
-        }
+        for (int v = 0; v < NV; ++v) s = dot4(l1[v], rw[d][v], s);
         pd[d] = s;
       }
       wave_reduce_multi<NT>(pd, dot, lane);
@@ -390,12 +464,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
         if (prev_dirty) {
           double s = 0.0;
 #pragma unroll
-          for (int v = 0; v < NV; ++v) {
-            s = fma((double)l1[v].x, (double)rw[d][v].x, s);
-            s = fma((double)l1[v].y, (double)rw[d][v].y, s);
-            s = fma((double)l1[v].z, (double)rw[d][v].z, s);
-            s = fma((double)l1[v].w, (double)rw[d][v].w, s);
-          }
+          for (int v = 0; v < NV; ++v) s = dot4(l1[v], rw[d][v], s);
           dt = wave_allreduce_d(s);
           dirty[d] = true;
         }
@@ -414,54 +483,277 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
           rw[d][v].z = __fmaf_rn(g, l1[v].z, rw[d][v].z);
           rw[d][v].w = __fmaf_rn(g, l1[v].w, rw[d][v].w);
         }
+        if (tg[d] < hot) {
+          float* row = a.wr1 + (int64_t)tg[d] * a.ld + lane;
+#pragma unroll
+          for (int i = 0; i < NE; ++i)
+            if (eon[i]) atomicAdd(row + 64 * i, g * l1e[i]);
+        }
         dirty[d] = true;
         any = true;
       }
 
-      // write-back: each touched syn1neg row once (its last occurrence)
+      // write-back: each touched cold syn1neg row once (its last occurrence)
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         bool later = false;
 #pragma unroll
         for (int d2 = d + 1; d2 < NT; ++d2) later |= (tg[d2] == tg[d]);
-        if (!dirty[d] || later) continue;
-        const int64_t tb = (int64_t)tg[d] * ld4 + lane;
+        if (!dirty[d] || later || tg[d] < hot) continue;
+        const int off = tg[d] * rowb + lane * 16;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           if (!on[v]) continue;
           if (MODE == kModeMinibatch) {
-            const float4 o = rd1[tb + 64 * v];
-            float* p = reinterpret_cast<float*>(&wr1[tb + 64 * v]);
+            const float4 o = bload4<0>(r1, off + 1024 * v);
+            float* p = a.wr1 + (int64_t)tg[d] * a.ld + (lane + 64 * v) * 4;
             atomicAdd(p + 0, rw[d][v].x - o.x);
             atomicAdd(p + 1, rw[d][v].y - o.y);
             atomicAdd(p + 2, rw[d][v].z - o.z);
             atomicAdd(p + 3, rw[d][v].w - o.w);
           } else {
-            wr1[tb + 64 * v] = rw[d][v];
+            bstore4<SA>(w1, off + 1024 * v, rw[d][v]);
           }
         }
       }
       if (any) {
         const float lf = a.lockf[input];
+        if (input < hot) {
+          // transpose work to element layout through LDS, then coalesced atomics
+          float* sw = s_work[wid];
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          if (!on[v]) continue;
-          float4 o;
-          o.x = __fmaf_rn(lf, work[v].x, l1[v].x);
-          o.y = __fmaf_rn(lf, work[v].y, l1[v].y);
-          o.z = __fmaf_rn(lf, work[v].z, l1[v].z);
-          o.w = __fmaf_rn(lf, work[v].w, l1[v].w);
-          if (MODE == kModeMinibatch) {
-            float* p = reinterpret_cast<float*>(&wr0[in_base + 64 * v]);
-            atomicAdd(p + 0, o.x - l1[v].x);
-            atomicAdd(p + 1, o.y - l1[v].y);
-            atomicAdd(p + 2, o.z - l1[v].z);
-            atomicAdd(p + 3, o.w - l1[v].w);
-          } else {
-            wr0[in_base + 64 * v] = o;
+          for (int v = 0; v < NV; ++v)
+            *reinterpret_cast<float4*>(sw + (lane + 64 * v) * 4) = work[v];
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+          float* row = a.wr0 + (int64_t)input * a.ld + lane;
+#pragma unroll
+          for (int i = 0; i < NE; ++i)
+            if (eon[i]) atomicAdd(row + 64 * i, lf * sw[lane + 64 * i]);
+          __builtin_amdgcn_wave_barrier();
+        } else {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            if (!on[v]) continue;
+            float4 o;
+            o.x = __fmaf_rn(lf, work[v].x, l1[v].x);
+            o.y = __fmaf_rn(lf, work[v].y, l1[v].y);
+            o.z = __fmaf_rn(lf, work[v].z, l1[v].z);
+            o.w = __fmaf_rn(lf, work[v].w, l1[v].w);
+            if (MODE == kModeMinibatch) {
+              float* p = a.wr0 + (int64_t)input * a.ld + (lane + 64 * v) * 4;
+              atomicAdd(p + 0, o.x - l1[v].x);
+              atomicAdd(p + 1, o.y - l1[v].y);
+              atomicAdd(p + 2, o.z - l1[v].z);
+              atomicAdd(p + 3, o.w - l1[v].w);
+            } else {
+              bstore4<SA>(w0, in_off + 1024 * v, o);
+            }
           }
         }
       }
+    }
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// k_sgns_atomic: the production Hogwild kernel
+// ---------------------------------------------------------------------------
+// Same per-example math as k_sgns, but every table update is a memory-side
+// float atomic of the delta (g * syn0[input] into syn1neg[t], lockf * work
+// into syn0[input]).  With ~4k examples in flight on 256 CUs every row of a
+// 24k-gene vocabulary is touched every few microseconds, so plain
+// read-modify-write stores lose most updates (measured: iteration-0 loss 4.15
+// vs 2.77 sequential); atomics keep all of them (2.76).
+//
+// Pipelining: example e+1's record and rows are loaded BEFORE example e's
+// atomics are issued, so the loads never wait behind the atomics in the
+// wave's in-order vmcnt.  l1 and work are staged through LDS in element order
+// so each atomic wave-instruction adds 64 contiguous floats (256 B); the
+// D % 64 tails of all K+2 rows are packed into shared instructions.
+template <int K, int NV>
+struct ExRegs {
+  int32_t tg[K + 1];
+  int32_t input;
+  float alpha;
+  float4 l1[NV];
+  float4 rw[K + 1][NV];
+};
+
+template <int K, int NV>
+__device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a, int64_t e,
+                                             __amdgpu_buffer_rsrc_t r0,
+                                             __amdgpu_buffer_rsrc_t r1, int rowb, int lane,
+                                             const bool (&on)[NV]) {
+  const int32_t* r = a.rec + e * a.rec_stride;
+  x.tg[0] = __builtin_amdgcn_readfirstlane(r[0]);
+  x.input = __builtin_amdgcn_readfirstlane(r[1]);
+  x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
+#pragma unroll
+  for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
+  const int in_off = x.input * rowb + lane * 16;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    x.l1[v] = on[v] ? bload4<0>(r0, in_off + 1024 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int d = 0; d <= K; ++d) {
+    const int off = (x.tg[d] < 0 ? 0 : x.tg[d]) * rowb + lane * 16;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+      x.rw[d][v] = (on[v] && x.tg[d] >= 0) ? bload4<0>(r1, off + 1024 * v)
+                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+template <int K, int NV>
+__global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
+  constexpr int NT = K + 1;
+  constexpr int W = kSgnsThreads / 64;
+  __shared__ float s_lut[kExpTableSize];
+  __shared__ float s_l1[W][256 * NV];
+  __shared__ float s_wk[W][256 * NV];
+  for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) s_lut[i] = a.exp_table[i];
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int64_t gw = (int64_t)blockIdx.x * W + wid;
+  const int64_t nw = (int64_t)gridDim.x * W;
+  const int64_t E = *a.n_examples;
+  const int D = a.D;
+  const int full = D >> 6;           // whole 64-float atomic groups per row
+  const int tail = D & 63;           // leftover floats per row
+  const int tpack = tail ? 64 / tail : 0;  // row tails per packed instruction
+  const int64_t tbytes = (int64_t)a.V * a.ld * 4;
+  const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.rd0, tbytes);
+  const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.rd1, tbytes);
+  const int rowb = (int)a.ld * 4;
+  float* S0 = a.wr0;
+  float* S1 = a.wr1;
+  float* s1 = s_l1[wid];
+  float* sw = s_wk[wid];
+  bool on[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) on[v] = (lane + 64 * v) < a.nvec;
+
+  for (int64_t c = gw; c * kChunk < E; c += nw) {
+    const int64_t e_beg = c * kChunk;
+    const int64_t e_end = (e_beg + kChunk < E) ? e_beg + kChunk : E;
+    ExRegs<K, NV> x;
+    load_example<K, NV>(x, a, e_beg, r0, r1, rowb, lane, on);
+    for (int64_t e = e_beg; e < e_end; ++e) {
+      // ---- compute example e ------------------------------------------------
+      double pd[NT], dot[NT];
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        double s = 0.0;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) s = dot4(x.l1[v], x.rw[d][v], s);
+        pd[d] = s;
+      }
+      wave_reduce_multi<NT>(pd, dot, lane);
+      float4 work[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) work[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      float g[NT];
+      bool dirty[NT];
+      bool any = false;
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        g[d] = 0.f;
+        dirty[d] = false;
+        if (x.tg[d] < 0) continue;
+        double dt = dot[d];
+        bool prev_dirty = false;
+#pragma unroll
+        for (int d2 = 0; d2 < d; ++d2) {
+          if (x.tg[d2] == x.tg[d]) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v) x.rw[d][v] = x.rw[d2][v];
+            prev_dirty = dirty[d2];
+          }
+        }
+        if (prev_dirty) {
+          double s = 0.0;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) s = dot4(x.l1[v], x.rw[d][v], s);
+          dt = wave_allreduce_d(s);
+          dirty[d] = true;
+        }
+        const float f = (float)dt;
+        if (f <= -(float)kMaxExp || f >= (float)kMaxExp) continue;
+        const int idx = (int)((f + (float)kMaxExp) * (float)kLutScale);
+        const float gg = ((d == 0 ? 1.0f : 0.0f) - s_lut[idx]) * x.alpha;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          work[v].x = __fmaf_rn(gg, x.rw[d][v].x, work[v].x);
+          work[v].y = __fmaf_rn(gg, x.rw[d][v].y, work[v].y);
+          work[v].z = __fmaf_rn(gg, x.rw[d][v].z, work[v].z);
+          work[v].w = __fmaf_rn(gg, x.rw[d][v].w, work[v].w);
+          x.rw[d][v].x = __fmaf_rn(gg, x.l1[v].x, x.rw[d][v].x);
+          x.rw[d][v].y = __fmaf_rn(gg, x.l1[v].y, x.rw[d][v].y);
+          x.rw[d][v].z = __fmaf_rn(gg, x.l1[v].z, x.rw[d][v].z);
+          x.rw[d][v].w = __fmaf_rn(gg, x.l1[v].w, x.rw[d][v].w);
+        }
+        g[d] = gg;
+        dirty[d] = true;
+        any = true;
+      }
+      // stage l1 / work in element order
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        *reinterpret_cast<float4*>(s1 + (lane + 64 * v) * 4) = x.l1[v];
+        *reinterpret_cast<float4*>(sw + (lane + 64 * v) * 4) = work[v];
+      }
+      __builtin_amdgcn_wave_barrier();
+      int32_t tg[NT];
+#pragma unroll
+      for (int d = 0; d < NT; ++d) tg[d] = x.tg[d];
+      const int32_t input = x.input;
+      const float lf = any ? a.lockf[input] : 0.f;
+
+      // ---- prefetch example e+1 (its loads overtake e's atomics) -------------
+      if (e + 1 < e_end) load_example<K, NV>(x, a, e + 1, r0, r1, rowb, lane, on);
+
+      // ---- atomics of example e -----------------------------------------------
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        if (g[d] == 0.f) continue;
+        float* row = S1 + (int64_t)tg[d] * a.ld + lane;
+        for (int i = 0; i < full; ++i) atomicAdd(row + 64 * i, g[d] * s1[64 * i + lane]);
+      }
+      if (any) {
+        float* row = S0 + (int64_t)input * a.ld + lane;
+        for (int i = 0; i < full; ++i) atomicAdd(row + 64 * i, lf * sw[64 * i + lane]);
+      }
+      if (tail) {
+        // rows q = 0..K: syn1neg[tg[q]] += g[q] * l1; q = K+1: syn0[input] += lf * work
+        for (int q0 = 0; q0 < NT + 1; q0 += tpack) {
+          const int q = q0 + lane / tail;
+          const int el = full * 64 + lane % tail;
+          float coef = 0.f;
+          int64_t base = 0;
+          bool from_work = false;
+#pragma unroll
+          for (int d = 0; d < NT; ++d) {
+            if (q == d) {
+              coef = g[d];
+              base = (int64_t)(tg[d] < 0 ? 0 : tg[d]) * a.ld;
+            }
+          }
+          if (q == NT) {
+            coef = any ? lf : 0.f;
+            base = (int64_t)input * a.ld;
+            from_work = true;
+          }
+          if (lane / tail < tpack && q <= NT && coef != 0.f) {
+            const float src = from_work ? sw[el] : s1[el];
+            atomicAdd((from_work ? S0 : S1) + base + el, coef * src);
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -547,25 +839,42 @@ hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
   return hipGetLastError();
 }
 
-template <int K, int NV>
-static hipError_t launch_sgns_kn(const SgnsArgs& a, int mode, int grid, hipStream_t st) {
+template <int K, int NV, int POL>
+static hipError_t launch_sgns_knp(const SgnsArgs& a, int mode, int grid, hipStream_t st) {
   switch (mode) {
     case kModeSequential:
-      hipLaunchKernelGGL((k_sgns<K, NV, kModeSequential>), dim3(1), dim3(kSgnsThreads), 0, st, a);
+      hipLaunchKernelGGL((k_sgns<K, NV, kModeSequential, POL>), dim3(1), dim3(kSgnsThreads), 0, st,
+                         a);
       break;
     case kModeMinibatch:
-      hipLaunchKernelGGL((k_sgns<K, NV, kModeMinibatch>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+      hipLaunchKernelGGL((k_sgns<K, NV, kModeMinibatch, POL>), dim3(grid), dim3(kSgnsThreads), 0,
+                         st, a);
       break;
     default:
-      hipLaunchKernelGGL((k_sgns<K, NV, kModeHogwild>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+      hipLaunchKernelGGL((k_sgns<K, NV, kModeHogwild, POL>), dim3(grid), dim3(kSgnsThreads), 0, st,
+                         a);
   }
   return hipGetLastError();
 }
 
+template <int K, int NV>
+static hipError_t launch_sgns_kn(const SgnsArgs& a, int mode, int pol, int grid, hipStream_t st) {
+  if (mode == kModeHogwild && a.hot_rows >= a.V) {
+    hipLaunchKernelGGL((k_sgns_atomic<K, NV>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  // sequential / minibatch are parity modes: default policy only
+  if (mode == kModeSequential || mode == kModeMinibatch || pol == kPolPlain)
+    return launch_sgns_knp<K, NV, kPolPlain>(a, mode, grid, st);
+  if (pol == kPolWtRd) return launch_sgns_knp<K, NV, kPolWtRd>(a, mode, grid, st);
+  return launch_sgns_knp<K, NV, kPolWt>(a, mode, grid, st);
+}
+
 template <int K>
-static hipError_t launch_sgns_k(const SgnsArgs& a, int nv, int mode, int grid, hipStream_t st) {
-  if (nv == 1) return launch_sgns_kn<K, 1>(a, mode, grid, st);
-  return launch_sgns_kn<K, 2>(a, mode, grid, st);
+static hipError_t launch_sgns_k(const SgnsArgs& a, int nv, int mode, int pol, int grid,
+                                hipStream_t st) {
+  if (nv == 1) return launch_sgns_kn<K, 1>(a, mode, pol, grid, st);
+  return launch_sgns_kn<K, 2>(a, mode, pol, grid, st);
 }
 
 bool sgns_supported(int K, int nv) {
@@ -576,15 +885,16 @@ bool sgns_supported(int K, int nv) {
   }
 }
 
-hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int grid, hipStream_t st) {
+hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int pol, int grid,
+                       hipStream_t st) {
   switch (K) {
-    case 1: return launch_sgns_k<1>(a, nv, mode, grid, st);
-    case 2: return launch_sgns_k<2>(a, nv, mode, grid, st);
-    case 3: return launch_sgns_k<3>(a, nv, mode, grid, st);
-    case 5: return launch_sgns_k<5>(a, nv, mode, grid, st);
-    case 10: return launch_sgns_k<10>(a, nv, mode, grid, st);
-    case 15: return launch_sgns_k<15>(a, nv, mode, grid, st);
-    case 20: return launch_sgns_k<20>(a, nv, mode, grid, st);
+    case 1: return launch_sgns_k<1>(a, nv, mode, pol, grid, st);
+    case 2: return launch_sgns_k<2>(a, nv, mode, pol, grid, st);
+    case 3: return launch_sgns_k<3>(a, nv, mode, pol, grid, st);
+    case 5: return launch_sgns_k<5>(a, nv, mode, pol, grid, st);
+    case 10: return launch_sgns_k<10>(a, nv, mode, pol, grid, st);
+    case 15: return launch_sgns_k<15>(a, nv, mode, pol, grid, st);
+    case 20: return launch_sgns_k<20>(a, nv, mode, pol, grid, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -594,7 +904,7 @@ int sgns_blocks_per_cu(int K, int nv) {
   hipError_t e = hipErrorInvalidValue;
 #define G2V_OCC(KK, NN)                                                                  \
   if (K == KK && nv == NN)                                                               \
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sgns<KK, NN, kModeHogwild>, \
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_sgns_atomic<KK, NN>,           \
                                                      kSgnsThreads, 0);
   G2V_OCC(1, 1) G2V_OCC(2, 1) G2V_OCC(3, 1) G2V_OCC(5, 1) G2V_OCC(10, 1) G2V_OCC(15, 1)
   G2V_OCC(20, 1) G2V_OCC(1, 2) G2V_OCC(2, 2) G2V_OCC(3, 2) G2V_OCC(5, 2) G2V_OCC(10, 2)

@@ -109,6 +109,9 @@ class SGNSEngine:
         except Exception:
             pass
 
+    def set_option(self, key, value):
+        N.check(self._lib.g2v_set_option(self._h, key, int(value)))
+
     def set_stream(self, stream_handle):
         N.check(self._lib.g2v_set_stream(self._h, C.c_void_p(stream_handle or 0)))
 

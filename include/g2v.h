@@ -88,6 +88,22 @@ int g2v_destroy(g2v_ctx *ctx);
 /* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
  * NULL restores the context's own stream. */
 int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
+/* Tuning knobs (defaults in brackets):
+ *   G2V_OPT_HOT_ROWS      rows [0, n) -- the n most frequent genes -- are updated
+ *                         with memory-side float atomics, the rest with plain
+ *                         stores; -1 = all rows [-1]
+ *   G2V_OPT_CACHE_POLICY  0 default, 1 write-through stores (sc1), 2 sc1 loads and
+ *                         stores [1]
+ *   G2V_OPT_SEG_JOBS      gensim jobs per sampling/update segment [1024]
+ *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = CUs x occupancy [0]
+ *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
+ *                         2 uncached (re-allocates, zero-filled) [0] */
+#define G2V_OPT_HOT_ROWS 1
+#define G2V_OPT_CACHE_POLICY 2
+#define G2V_OPT_SEG_JOBS 3
+#define G2V_OPT_GRID 4
+#define G2V_OPT_TABLE_MEM 5
+int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);
 
