@@ -1,0 +1,258 @@
+#!/usr/bin/env python
+"""Benchmark: gene pairs/sec of the Gene2vec SGNS hot path on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): synthetic Zipf(1.0) gene pairs over
+V = 24,447 genes, 100 M pairs per GPU, dim 200, negative 5, window 1,
+sample 1e-3, alpha 0.025 -> 1e-4 restarting every step.  One STEP = one
+gensim train() call = one epoch over the GPU's pairs (src/gene2vec.py:87),
+i.e. downsampling + negative sampling + SGNS updates for every pair.  Inputs
+(token ids, tables, job schedule) are resident in HBM before timing starts.
+
+N > 1 (torchrun, one rank per GPU, RCCL over xGMI): weak scaling, each rank
+trains its own 125 M-pair shard (BASELINE configs[2]: 1 B pairs over 8 GPUs)
+on a replica of the tables, and the replicas are averaged with
+torch.distributed.all_reduce(AVG) every --avg-every-jobs jobs.
+
+Prints ONE JSON line on rank 0 (see the contract in the task description):
+value = pairs/s over all ranks, plus `roofline` (dominant kernel =
+k_sgns_atomic, algorithmic bytes 2*(K+2)*D*4 per directed example / its
+average launch time, HIP events on the launch stream) and `cpu_baseline`
+(the C oracle, Hogwild OpenMP, on a bounded sample of the same corpus).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+import zlib
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+METRIC = "gene pairs/sec (SGNS dim200 neg5) at 1/2/4/8 MI355X + achieved GB/s"
+HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--pairs", type=int, default=0, help="pairs per GPU (0 = 100M at N=1, 125M at N>1)")
+    p.add_argument("--vocab", type=int, default=24447)
+    p.add_argument("--dim", type=int, default=200)
+    p.add_argument("--negative", type=int, default=5)
+    p.add_argument("--sample", type=float, default=1e-3)
+    p.add_argument("--zipf", type=float, default=1.0)
+    p.add_argument("--avg-every-jobs", type=int, default=5000, help="RCCL averaging cadence (N>1)")
+    p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
+    p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-eval", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    from gene2vec_amd import _native as N
+    from gene2vec_amd import engine as E
+    from gene2vec_amd import synthetic as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    n_pairs = a.pairs or (100_000_000 if world == 1 else 125_000_000)
+    V0, D, K = a.vocab, a.dim, a.negative
+
+    # ---- corpus shard + global vocabulary ---------------------------------------
+    t = time.time()
+    pairs = S.zipf_gene_pairs(n_pairs, V0, a.zipf, seed=20250114, shard=rank)
+    flat = pairs.reshape(-1)
+    counts, first = E.count_ids(flat, V0)
+    if world > 1:
+        c_t = torch.from_numpy(counts).to(dev)
+        dist.all_reduce(c_t)
+        first_g = np.where(first >= 0, first + rank * flat.size, np.iinfo(np.int64).max)
+        f_t = torch.from_numpy(first_g).to(dev)
+        dist.all_reduce(f_t, op=dist.ReduceOp.MIN)
+        counts, first = c_t.cpu().numpy(), f_t.cpu().numpy()
+    order, remap = S.vocab_order(counts, first)
+    V = len(order)
+    vcounts = counts[order].astype(np.int64)
+    tok = remap[flat]
+    del flat, pairs
+    t_corpus = time.time() - t
+
+    # ---- device state --------------------------------------------------------------
+    eng = E.SGNSEngine(V, D, K, device=local)
+    if a.grid:
+        eng.set_option(N.OPT_GRID, a.grid)
+    # a dedicated (non-default) stream: g2v kernels, RCCL all-reduces and the
+    # timing events are all ordered on it
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    assert stream.cuda_stream != 0
+    eng.set_stream(stream.cuda_stream)
+    ld = eng.ld
+    names = S.gene_names(V0)
+    seeds = np.array([zlib.crc32((names[i] + "1").encode()) for i in order], np.uint32)
+    syn0_h = E.seeded_vectors(seeds, D)  # [ext] seeded_vector, deterministic hash
+    syn0 = torch.zeros((V, ld), dtype=torch.float32, device=dev)
+    syn1 = torch.zeros((V, ld), dtype=torch.float32, device=dev)
+    syn0[:, :D] = torch.from_numpy(syn0_h).to(dev)
+    eng.bind_tables(syn0.data_ptr(), syn1.data_ptr(), ld, keepalive=(syn0, syn1))
+    eng.set_vocab(vcounts, a.sample)
+    tok_d = torch.from_numpy(tok).to(dev)
+    eng.set_corpus_device(tok_d.data_ptr(), tok_d.numel(), sent_len=2, keepalive=tok_d)
+    js = E.plan_jobs(n_sent=n_pairs, sent_len=2)
+    n_jobs = len(js) - 1
+    alphas = E.job_alphas(js, n_pairs)
+    rs = np.random.RandomState(1 + rank)  # gensim model.random(seed=1); one stream per rank
+    step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
+    avg_every = max(1, a.avg_every_jobs) if world > 1 else n_jobs
+    torch.cuda.synchronize(dev)
+
+    def step(i, timing):
+        for j0 in range(0, n_jobs, avg_every):
+            j1 = min(n_jobs, j0 + avg_every)
+            eng.train(js[j0:j1 + 1], alphas[j0:j1], step_seeds[i][j0:j1], N.MODE_HOGWILD,
+                      timing=timing)
+            if world > 1:
+                dist.all_reduce(syn0, op=dist.ReduceOp.AVG)
+                dist.all_reduce(syn1, op=dist.ReduceOp.AVG)
+
+    for i in range(a.warmup):
+        step(i, False)
+    torch.cuda.synchronize(dev)
+    eng.read_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    w0 = time.perf_counter()
+    ev0.record(stream)
+    for i in range(a.steps):
+        step(a.warmup + i, True)
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - w0
+    st = eng.read_stats()
+    gpu_ms = ev0.elapsed_time(ev1)
+    elapsed = max(wall, gpu_ms / 1e3)
+    if world > 1:
+        el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+        ex = torch.tensor([st["examples"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(ex)
+        total_examples = int(ex.item())
+    else:
+        total_examples = st["examples"]
+    total_pairs = n_pairs * a.steps * world
+    value = total_pairs / elapsed
+
+    # ---- roofline of the dominant kernel (k_sgns_atomic) --------------------------------
+    bytes_per_example = 2 * (K + 2) * D * 4
+    launches = max(1, st["launches"])
+    avg_launch_ms = st["sgns_kernel_ms"] / launches
+    alg_bytes_launch = st["examples"] * bytes_per_example / launches
+    achieved = alg_bytes_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms > 0 else 0.0
+    traffic = None
+    if os.path.exists(a.traffic_json):
+        try:
+            tj = json.load(open(a.traffic_json))
+            if tj.get("vocab") == V0 and tj.get("dim") == D and tj.get("negative") == K:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+                "kernel": "k_sgns_atomic", "avg_launch_ms": round(avg_launch_ms, 4),
+                "algorithmic_bytes_per_launch": int(alg_bytes_launch),
+                "bytes_per_example": bytes_per_example}
+
+    # ---- quality sanity check: SGNS objective on held-in pairs ------------------------------
+    quality = None
+    if not a.no_eval and rank == 0:
+        s0 = syn0[:, :D].cpu().numpy()
+        s1 = syn1[:, :D].cpu().numpy()
+        r = np.random.Generator(np.random.PCG64(99))
+        idx = r.integers(0, n_pairs, 20000)
+        c, j = tok[2 * idx], tok[2 * idx + 1]
+        p = vcounts.astype(np.float64) ** 0.75
+        negs = r.choice(V, size=(20000, K), p=p / p.sum())
+        u = s0[j].astype(np.float64)
+        pos = np.einsum("nd,nd->n", u, s1[c].astype(np.float64))
+        neg = np.einsum("nd,nkd->nk", u, s1[negs].astype(np.float64))
+        loss = float((np.logaddexp(0, -pos) + np.logaddexp(0, neg).sum(1)).mean())
+        quality = {"sgns_loss_heldin": round(loss, 4), "init_loss": round((K + 1) * np.log(2), 4)}
+
+    # ---- CPU baseline (C oracle, Hogwild OpenMP) on a bounded sample -------------------------
+    cpu = None
+    if world == 1 and not a.no_cpu_baseline:
+        from oracle import c_oracle as CO
+        ncpu = a.cpu_threads or min(16, os.cpu_count() or 1)
+        ns = min(a.cpu_sample_pairs, n_pairs)
+        jsc = E.plan_jobs(n_sent=ns, sent_len=2)
+        off = np.arange(0, 2 * ns + 1, 2, dtype=np.int64)
+        c0 = syn0_h.copy()
+        c1 = np.zeros_like(c0)
+        si = CO.sample_int(vcounts, a.sample)
+        cum = CO.make_cum_table(vcounts)
+        al = E.job_alphas(jsc, ns).astype(np.float32)
+        sd = E.job_seeds(np.random.RandomState(1), len(jsc) - 1)
+        t = time.perf_counter()
+        CO.train(tok[:2 * ns], off, jsc, al, sd, si, a.sample != 0, cum, c0, c1,
+                 np.ones(V, np.float32), K, nthreads=ncpu)
+        dt = time.perf_counter() - t
+        cpu = {"value": round(ns / dt, 1), "unit": "pairs/s", "cores": ncpu, "kind": "port",
+               "sample": f"first {ns} pairs of the same corpus, 1 epoch, C oracle "
+                         f"(oracle/sgns_oracle.c) Hogwild OpenMP, {dt:.2f} s"}
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "pairs/s", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {
+                "workload": ("C2: synthetic Zipf(1.0) gene pairs, V=24447, 100M pairs, dim 200, "
+                             "neg 5, window 1, sample 1e-3, 1 epoch per step") if world == 1 else
+                            (f"C3: synthetic Zipf gene pairs, V=24447, {n_pairs} pairs per GPU x "
+                             f"{world}, dim 200, neg 5, RCCL model averaging every "
+                             f"{avg_every} jobs"),
+                "vocab": V, "pairs_per_gpu": n_pairs, "dim": D, "negative": K,
+                "sample": a.sample, "window": 1,
+                "parallelism": f"dp{world}" + (" + RCCL AVG all-reduce" if world > 1 else "")},
+            "examples_per_s": round(total_examples / elapsed, 1),
+            "effective_examples": total_examples,
+            "roofline": roofline, "cpu_baseline": cpu, "quality": quality,
+            "gpu_event_ms": round(gpu_ms, 3), "wall_s": round(wall, 4),
+            "corpus_gen_s": round(t_corpus, 2),
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
