@@ -65,6 +65,7 @@ def main():
     import torch.distributed as dist
 
     from gene2vec_amd import _native as N
+    from gene2vec_amd import distributed as Dd
     from gene2vec_amd import engine as E
     from gene2vec_amd import synthetic as S
 
@@ -84,13 +85,7 @@ def main():
     pairs = S.zipf_gene_pairs(n_pairs, V0, a.zipf, seed=20250114, shard=rank)
     flat = pairs.reshape(-1)
     counts, first = E.count_ids(flat, V0)
-    if world > 1:
-        c_t = torch.from_numpy(counts).to(dev)
-        dist.all_reduce(c_t)
-        first_g = np.where(first >= 0, first + rank * flat.size, np.iinfo(np.int64).max)
-        f_t = torch.from_numpy(first_g).to(dev)
-        dist.all_reduce(f_t, op=dist.ReduceOp.MIN)
-        counts, first = c_t.cpu().numpy(), f_t.cpu().numpy()
+    counts, first = Dd.global_vocab(counts, first, token_offset=rank * flat.size, device=dev)
     order, remap = S.vocab_order(counts, first)
     V = len(order)
     vcounts = counts[order].astype(np.int64)
@@ -122,19 +117,14 @@ def main():
     js = E.plan_jobs(n_sent=n_pairs, sent_len=2)
     n_jobs = len(js) - 1
     alphas = E.job_alphas(js, n_pairs)
-    rs = np.random.RandomState(1 + rank)  # gensim model.random(seed=1); one stream per rank
+    rs = np.random.RandomState(Dd.rank_seed(1, rank))  # gensim model.random(seed=1) per rank
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     avg_every = max(1, a.avg_every_jobs) if world > 1 else n_jobs
+    trainer = Dd.ReplicaTrainer(eng, (syn0, syn1), avg_every, N.MODE_HOGWILD)
     torch.cuda.synchronize(dev)
 
     def step(i, timing):
-        for j0 in range(0, n_jobs, avg_every):
-            j1 = min(n_jobs, j0 + avg_every)
-            eng.train(js[j0:j1 + 1], alphas[j0:j1], step_seeds[i][j0:j1], N.MODE_HOGWILD,
-                      timing=timing)
-            if world > 1:
-                dist.all_reduce(syn0, op=dist.ReduceOp.AVG)
-                dist.all_reduce(syn1, op=dist.ReduceOp.AVG)
+        trainer.train_epoch(js, alphas, step_seeds[i], timing=timing)
 
     for i in range(a.warmup):
         step(i, False)

@@ -93,6 +93,7 @@ struct g2v_ctx {
   int cus = 0, sgns_grid = 0;
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
+  int debug_write = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
 
   float *own0 = nullptr, *own1 = nullptr;  // context-owned tables
@@ -345,6 +346,10 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       }
       return G2V_OK;
     }
+    case G2V_OPT_DEBUG_WRITE:
+      REQUIRE(value >= 0 && value <= 2, G2V_EINVAL, "debug write mode out of [0, 2]");
+      c->debug_write = (int)value;
+      return G2V_OK;
     case G2V_OPT_GRID:
       REQUIRE(value >= 0, G2V_EINVAL, "grid must be >= 0");
       c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv);
@@ -609,6 +614,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.V = c->V;
   s.hot_rows = c->hot_rows < 0 ? c->V : std::min(c->hot_rows, c->V);
   s.exp_table = c->exp_table;
+  s.debug_write = c->debug_write;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc;
   if (timing) {

@@ -74,6 +74,7 @@ struct SgnsArgs {
   int D;
   int V;
   int hot_rows;             // rows [0, hot_rows) are updated with float atomics
+  int debug_write;          // ablation: 0 atomics, 1 plain stores, 2 no writes
   const float* exp_table;   // [1000]
 };
 

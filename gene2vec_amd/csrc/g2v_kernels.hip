@@ -606,7 +606,15 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
   }
 }
 
-template <int K, int NV>
+// WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
+// 2 no table writes
+template <int WR>
+__device__ __forceinline__ void upd(float* p, float v) {
+  if (WR == 0) atomicAdd(p, v);
+  else if (WR == 1) *p = v;
+}
+
+template <int K, int NV, int WR = 0>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
@@ -721,11 +729,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       for (int d = 0; d < NT; ++d) {
         if (g[d] == 0.f) continue;
         float* row = S1 + (int64_t)tg[d] * a.ld + lane;
-        for (int i = 0; i < full; ++i) atomicAdd(row + 64 * i, g[d] * s1[64 * i + lane]);
+        for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, g[d] * s1[64 * i + lane]);
       }
       if (any) {
         float* row = S0 + (int64_t)input * a.ld + lane;
-        for (int i = 0; i < full; ++i) atomicAdd(row + 64 * i, lf * sw[64 * i + lane]);
+        for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, lf * sw[64 * i + lane]);
       }
       if (tail) {
         // rows q = 0..K: syn1neg[tg[q]] += g[q] * l1; q = K+1: syn0[input] += lf * work
@@ -749,7 +757,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           }
           if (lane / tail < tpack && q <= NT && coef != 0.f) {
             const float src = from_work ? sw[el] : s1[el];
-            atomicAdd((from_work ? S0 : S1) + base + el, coef * src);
+            upd<WR>((from_work ? S0 : S1) + base + el, coef * src);
           }
         }
       }
@@ -860,7 +868,12 @@ static hipError_t launch_sgns_knp(const SgnsArgs& a, int mode, int grid, hipStre
 template <int K, int NV>
 static hipError_t launch_sgns_kn(const SgnsArgs& a, int mode, int pol, int grid, hipStream_t st) {
   if (mode == kModeHogwild && a.hot_rows >= a.V) {
-    hipLaunchKernelGGL((k_sgns_atomic<K, NV>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    if (a.debug_write == 1 && K == 5 && NV == 1)
+      hipLaunchKernelGGL((k_sgns_atomic<K, NV, 1>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    else if (a.debug_write == 2 && K == 5 && NV == 1)
+      hipLaunchKernelGGL((k_sgns_atomic<K, NV, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_sgns_atomic<K, NV>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
   // sequential / minibatch are parity modes: default policy only

@@ -1,0 +1,127 @@
+"""CLI mirror of the reference's src/gene2vec.py.
+
+    python -m gene2vec_amd.gene2vec <data_dir> <export_dir> <ending_pattern> [options]
+
+Same positional arguments (src/gene2vec.py:8-15), same ingest (shuffled
+listdir, files ending with the pattern, windows-1252, line.strip().split(),
+one global shuffle; :29-55), same hyper-parameters (dim 200, 32 workers,
+skip-gram, 10 iterations, window 1; :57-63) and the same 10-iteration loop:
+iteration 1 builds the model with iter=1 (:70), iterations >= 2 reshuffle,
+reload the previous iteration's file and train one more epoch with alpha
+restarting at 0.025 (:76-92).  Every iteration writes
+``gene2vec_dim_<dim>_iter_<n>`` (own checkpoint format, replacing gensim's
+pickle), ``..._iter_<n>.txt`` (generateMatrix) and ``..._iter_<n>_w2v.txt``
+(word2vec text format read by evaluation_target_function.py).  Training runs
+on the GPU through libg2v.so.
+"""
+from __future__ import annotations
+
+import argparse
+import datetime
+import logging
+import os
+import random
+import zlib
+
+from . import generateMatrix as gM
+from .word2vec import Word2Vec
+
+
+def read_gene_pairs(source_dir, ending_pattern, rng=random):
+    """src/gene2vec.py:29-47: shuffled file order, windows-1252, strip().split()."""
+    files = os.listdir(source_dir)
+    size = len(files)
+    rng.shuffle(files)
+    gene_pairs = []
+    num_db = 0
+    for fname in files:
+        if not fname.endswith(ending_pattern):
+            continue
+        num_db += 1
+        print(datetime.datetime.now())
+        print("current file " + fname + " num: " + str(num_db) + " total files " + str(size))
+        with open(os.path.join(source_dir, fname), "r", encoding="windows-1252") as f:
+            for line in f:
+                gene_pairs.append(line.strip().split())
+    return gene_pairs
+
+
+def _hashfxn(name):
+    if name == "python":
+        return hash
+    if name == "crc32":
+        return lambda s: zlib.crc32(s.encode("utf-8"))
+    raise ValueError(name)
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser(
+        description="Please specify data directory, embedding output directory and data file "
+                    "ending pattern")
+    parser.add_argument("fileAddress", metavar="N", type=str, nargs="+",
+                        help="python -m gene2vec_amd.gene2vec data_directory output_directory txt")
+    parser.add_argument("--dim", type=int, default=200)
+    parser.add_argument("--workers", type=int, default=32)
+    parser.add_argument("--iters", type=int, default=10)
+    parser.add_argument("--window", type=int, default=1)
+    parser.add_argument("--negative", type=int, default=5)
+    parser.add_argument("--sample", type=float, default=1e-3)
+    parser.add_argument("--device", type=int, default=0)
+    parser.add_argument("--mode", choices=("hogwild", "sequential"), default="hogwild")
+    parser.add_argument("--shuffle-seed", type=int, default=None,
+                        help="seed Python's shuffles (the reference leaves them unseeded)")
+    parser.add_argument("--hash", choices=("python", "crc32"), default="python",
+                        help="seeded_vector hash (gensim default: Python's randomised hash)")
+    parser.add_argument("--no-txt", action="store_true")
+    parser.add_argument("--no-w2v", action="store_true")
+    parser.add_argument("--w2v-binary", action="store_true")
+    args = parser.parse_args(argv)
+    source_dir, export_dir, ending_pattern = args.fileAddress[:3]
+
+    logging.basicConfig(format="%(asctime)s : %(levelname)s : %(message)s", level=logging.INFO)
+    print("start!")
+    rng = random.Random(args.shuffle_seed) if args.shuffle_seed is not None else random
+    gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
+    print(datetime.datetime.now())
+    print("shuffle start " + str(len(gene_pairs)))
+    rng.shuffle(gene_pairs)
+    print(datetime.datetime.now())
+    print("shuffle done " + str(len(gene_pairs)))
+
+    dimension = args.dim
+    hashfxn = _hashfxn(args.hash)
+    os.makedirs(export_dir, exist_ok=True)
+    outputs = []
+    for current_iter in range(1, args.iters + 1):
+        name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
+        if current_iter == 1:
+            print(f"gene2vec dimension {dimension} iteration {current_iter} start")
+            model = Word2Vec(gene_pairs, size=dimension, window=args.window, min_count=1,
+                             workers=args.workers, iter=1, sg=1, negative=args.negative,
+                             sample=args.sample, hashfxn=hashfxn, device=args.device,
+                             mode=args.mode)
+        else:
+            print(datetime.datetime.now())
+            print("shuffle start " + str(len(gene_pairs)))
+            rng.shuffle(gene_pairs)
+            print(datetime.datetime.now())
+            print("shuffle done " + str(len(gene_pairs)))
+            print(f"gene2vec dimension {dimension} iteration {current_iter} start")
+            prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
+            model = Word2Vec.load(prev, device=args.device)
+            model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
+        model.save(name)
+        if not args.no_txt:
+            gM.outputTxt(name)
+        if not args.no_w2v:
+            model.wv.save_word2vec_format(name + "_w2v.txt", binary=False)
+            if args.w2v_binary:
+                model.wv.save_word2vec_format(name + "_w2v.bin", binary=True)
+        print(f"gene2vec dimension {dimension} iteration {current_iter} done")
+        outputs.append(name)
+        del model
+    return outputs
+
+
+if __name__ == "__main__":
+    main()

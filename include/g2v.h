@@ -97,12 +97,15 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_SEG_JOBS      gensim jobs per sampling/update segment [1024]
  *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = CUs x occupancy [0]
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
- *                         2 uncached (re-allocates, zero-filled) [0] */
+ *                         2 uncached (re-allocates, zero-filled) [0]
+ *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
+ *                         atomics, 2 no table writes [0] */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
 #define G2V_OPT_GRID 4
 #define G2V_OPT_TABLE_MEM 5
+#define G2V_OPT_DEBUG_WRITE 6
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);

@@ -1,0 +1,112 @@
+"""World-size-2 gloo tests (CPU) of the multi-GPU path: sharding, global
+vocabulary, replica averaging and the averaging cadence of ReplicaTrainer.
+The RCCL (nccl backend) run uses the same code with device tensors."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from gene2vec_amd import distributed as Dd
+from gene2vec_amd import engine as E
+from gene2vec_amd import synthetic as S
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class FakeEngine:
+    """stands in for SGNSEngine: every job adds (rank+1) * job_index to the tables"""
+
+    def __init__(self, tables, rank):
+        self.tables, self.rank, self.calls = tables, rank, []
+
+    def train(self, js, al, sd, mode, timing=False):
+        self.calls.append((int(js[0]), int(js[-1]), len(al), len(sd)))
+        for t in self.tables:
+            t += float((self.rank + 1) * len(al))
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = {}
+        # sharding of one synthetic corpus
+        n = 10001
+        s0, s1 = Dd.shard_range(n, rank, world)
+        pairs = S.zipf_gene_pairs(n, 500, seed=3)[s0:s1]
+        flat = pairs.reshape(-1)
+        c, f = E.count_ids(flat, 500)
+        gc, gf = Dd.global_vocab(c, f, token_offset=2 * s0)
+        out["counts"], out["first"] = gc, gf
+        # averaging
+        t = torch.full((4, 3), float(rank + 1))
+        Dd.average_([t])
+        out["avg"] = t.numpy()
+        # cadence: 10 jobs, average every 4 -> windows of 4, 4, 2
+        tabs = [torch.zeros(2, 2), torch.zeros(3)]
+        eng = FakeEngine(tabs, rank)
+        tr = Dd.ReplicaTrainer(eng, tabs, avg_every_jobs=4)
+        js = np.arange(0, 21, 2, dtype=np.int64)
+        tr.train_epoch(js, np.zeros(10), np.zeros(10, np.uint64))
+        out["calls"] = eng.calls
+        out["tables"] = [x.numpy() for x in tabs]
+        out["averages"] = tr.averages
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def results():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def test_shard_range_partitions():
+    for n in (0, 1, 7, 10001):
+        for w in (1, 2, 3, 8):
+            r = [Dd.shard_range(n, k, w) for k in range(w)]
+            assert r[0][0] == 0 and r[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(r, r[1:]))
+
+
+def test_global_vocab_equals_single_process(results):
+    pairs = S.zipf_gene_pairs(10001, 500, seed=3)
+    c, f = E.count_ids(pairs.reshape(-1), 500)
+    for r in (0, 1):
+        assert np.array_equal(results[r]["counts"], c)
+        assert np.array_equal(results[r]["first"], f)
+
+
+def test_average_is_mean(results):
+    for r in (0, 1):
+        assert np.allclose(results[r]["avg"], 1.5)
+
+
+def test_replica_trainer_cadence_and_consistency(results):
+    for r in (0, 1):
+        assert results[r]["calls"] == [(0, 8, 4, 4), (8, 16, 4, 4), (16, 20, 2, 2)]
+        assert results[r]["averages"] == 3
+    # window adds (rank+1)*jobs, then the mean over ranks: 1.5*4 + 1.5*4 + 1.5*2
+    for t0, t1 in zip(results[0]["tables"], results[1]["tables"]):
+        assert np.array_equal(t0, t1)
+        assert np.allclose(t0, 15.0)

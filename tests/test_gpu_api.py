@@ -1,0 +1,82 @@
+"""GPU: the gensim-shaped API and the CLI mirror end to end, against the
+oracle (sequential mode must reproduce gensim workers=1 order to 1e-5)."""
+import os
+import random
+import shutil
+
+import numpy as np
+import pytest
+
+from gene2vec_amd import KeyedVectors, Word2Vec
+from gene2vec_amd.gene2vec import main as cli_main
+from gene2vec_amd.gene2vec import read_gene_pairs
+from oracle import sgns_oracle as O
+from tests.conftest import GOLDEN
+from tests.helpers import crc_hash
+
+pytestmark = pytest.mark.gpu
+
+
+def test_word2vec_api_sequential_matches_golden(test_pairs):
+    """src/gene2vec.py:70 then two :87 calls == three gensim iterations"""
+    z = np.load(os.path.join(GOLDEN, "e2e_test_pairs_s1e-3.npz"))
+    m = Word2Vec(test_pairs, size=200, window=1, min_count=1, workers=32, iter=1, sg=1,
+                 hashfxn=crc_hash, mode="sequential")
+    for _ in range(2):
+        m.train(test_pairs, total_examples=m.corpus_count, epochs=m.iter)
+    np.testing.assert_allclose(m.wv.vectors, z["syn0"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(m.syn1neg, z["syn1neg"], rtol=1e-5, atol=1e-7)
+
+
+def test_save_load_continue_equals_uninterrupted(tmp_path, test_pairs):
+    """the resume path of src/gene2vec.py:86-88 (checkpoint carries RNG state)"""
+    a = Word2Vec(test_pairs, size=64, window=1, min_count=1, iter=1, sg=1, hashfxn=crc_hash,
+                 mode="sequential")
+    f = str(tmp_path / "it1")
+    a.save(f)
+    a.train(test_pairs, total_examples=a.corpus_count, epochs=a.iter)
+    b = Word2Vec.load(f)
+    b.mode = "sequential"
+    b.train(test_pairs, total_examples=b.corpus_count, epochs=b.iter)
+    np.testing.assert_array_equal(a.wv.vectors, b.wv.vectors)
+    np.testing.assert_array_equal(a.syn1neg, b.syn1neg)
+
+
+def test_cli_end_to_end_matches_oracle(tmp_path, test_pairs):
+    data = tmp_path / "data"
+    data.mkdir()
+    shutil.copy(os.path.join(GOLDEN, "test_pairs.txt"), data / "test.txt")
+    out = tmp_path / "emb"
+    iters = 3
+    outs = cli_main([str(data), str(out), "txt", "--iters", str(iters), "--mode", "sequential",
+                     "--hash", "crc32", "--shuffle-seed", "7", "--w2v-binary"])
+    assert len(outs) == iters
+    for n in range(1, iters + 1):
+        base = out / f"gene2vec_dim_200_iter_{n}"
+        for suf in ("", ".txt", "_w2v.txt", "_w2v.bin"):
+            assert (out / (base.name + suf)).exists()
+    # oracle replay of the same ingest + shuffles + 3 iterations
+    rng = random.Random(7)
+    pairs = read_gene_pairs(str(data), "txt", rng)
+    rng.shuffle(pairs)
+    voc = O.build_vocab(pairs, 1, 1e-3)
+    syn0, syn1, lockf = O.reset_weights(voc.index2word, 200, 1, crc_hash)
+    cum = O.make_cum_table(voc.counts)
+    rs = np.random.RandomState(1)
+    for it in range(iters):
+        if it:
+            rng.shuffle(pairs)
+        ids = O.sentences_to_ids(pairs, voc.word2index)
+        O.train_epoch_sequential(ids, voc, syn0, syn1, lockf, cum, 5, rs, sample=1e-3)
+    kv = KeyedVectors.load_word2vec_format(str(out / f"gene2vec_dim_200_iter_{iters}_w2v.txt"))
+    assert kv.index2word == voc.index2word
+    np.testing.assert_allclose(kv.vectors, syn0, rtol=1e-5, atol=1e-7)
+    kvb = KeyedVectors.load_word2vec_format(str(out / f"gene2vec_dim_200_iter_{iters}_w2v.bin"),
+                                            binary=True)
+    np.testing.assert_array_equal(kvb.vectors, kv.vectors)
+    # .txt matrix in first-occurrence order, parseable the way the consumers parse it
+    rows = [ln.split() for ln in open(out / f"gene2vec_dim_200_iter_{iters}.txt")]
+    assert [r[0] for r in rows] == voc.first_order
+    got = np.array([r[1:] for r in rows], dtype=np.float32)
+    np.testing.assert_allclose(got, syn0[[voc.word2index[w] for w in voc.first_order]],
+                               rtol=1e-5, atol=1e-7)
