@@ -30,6 +30,8 @@ OPT_SEG_JOBS = 3
 OPT_GRID = 4
 OPT_TABLE_MEM = 5
 OPT_DEBUG_WRITE = 6
+OPT_STRIPE_ROWS = 7
+OPT_STRIPE_COPIES = 8
 BATCH_WORDS = 10000
 MAX_DIM = 512
 SUPPORTED_NEGATIVE = (1, 2, 3, 5, 10, 15, 20)

@@ -94,6 +94,9 @@ struct g2v_ctx {
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
+  int stripe_rows = 8, stripe_copies = 8;
+  float* stripe = nullptr;
+  int64_t stripe_cap = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
 
   float *own0 = nullptr, *own1 = nullptr;  // context-owned tables
@@ -292,6 +295,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->snap0);
   dev_free(c->snap1);
   dev_free(c->d_counters);
+  dev_free(c->stripe);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
@@ -346,6 +350,14 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       }
       return G2V_OK;
     }
+    case G2V_OPT_STRIPE_ROWS:
+      REQUIRE(value >= 0 && value <= 65536, G2V_EINVAL, "stripe rows out of [0, 65536]");
+      c->stripe_rows = (int)value;
+      return G2V_OK;
+    case G2V_OPT_STRIPE_COPIES:
+      REQUIRE(value >= 1 && value <= 16, G2V_EINVAL, "stripe copies out of [1, 16]");
+      c->stripe_copies = (int)value;
+      return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
       REQUIRE(value >= 0 && value <= 2, G2V_EINVAL, "debug write mode out of [0, 2]");
       c->debug_write = (int)value;
@@ -615,6 +627,19 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.hot_rows = c->hot_rows < 0 ? c->V : std::min(c->hot_rows, c->V);
   s.exp_table = c->exp_table;
   s.debug_write = c->debug_write;
+  const bool striped = mode == kModeHogwild && s.hot_rows >= c->V && c->stripe_copies > 1 &&
+                       c->stripe_rows > 0;
+  s.stripe_rows = striped ? std::min(c->stripe_rows, c->V) : 0;
+  s.stripe_copies = striped ? c->stripe_copies : 1;
+  if (striped) {
+    const int64_t need = 2 * (int64_t)(s.stripe_copies - 1) * s.stripe_rows * c->ld;
+    if (need > c->stripe_cap) {
+      int rc2 = dev_reserve(c->stream, &c->stripe, &c->stripe_cap, need);
+      if (rc2) return rc2;
+      HIPCHK(hipMemsetAsync(c->stripe, 0, sizeof(float) * c->stripe_cap, c->stream));
+    }
+  }
+  s.stripe = c->stripe;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc;
   if (timing) {
@@ -622,6 +647,8 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipEventRecord(e0, c->stream));
   }
   HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
+  HIPCHK(launch_fold_stripes(c->syn0, c->syn1, c->stripe, s.stripe_rows, s.stripe_copies, c->ld,
+                             c->nvec, c->stream));
   if (timing) {
     HIPCHK(hipEventRecord(e1, c->stream));
     c->t_sgns.emplace_back(e0, e1);

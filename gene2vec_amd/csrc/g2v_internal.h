@@ -76,6 +76,11 @@ struct SgnsArgs {
   int hot_rows;             // rows [0, hot_rows) are updated with float atomics
   int debug_write;          // ablation: 0 atomics, 1 plain stores, 2 no writes
   const float* exp_table;   // [1000]
+  // hot-row striping (k_sgns_atomic): rows [0, stripe_rows) of each table have
+  // stripe_copies-1 extra copies; value = main + sum(copies), atomics spread
+  float* stripe;            // [2][stripe_copies-1][stripe_rows][ld]
+  int stripe_rows;
+  int stripe_copies;        // 1 = off
 };
 
 hipError_t launch_job_sample(bool write, const SampleArgs& a, int64_t n_jobs, hipStream_t st);
@@ -88,6 +93,8 @@ bool sgns_supported(int K, int nv);
 hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int pol, int grid,
                        hipStream_t st);
 int sgns_blocks_per_cu(int K, int nv);
+hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
+                               int64_t ld, int nvec, hipStream_t st);
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
                         double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
                         hipStream_t st);

@@ -581,6 +581,40 @@ struct ExRegs {
   float4 rw[K + 1][NV];
 };
 
+// row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
+// main row plus its stripe copies when t is a striped hot row
+template <int NV>
+__device__ __forceinline__ void load_row(float4 (&o)[NV], const SgnsArgs& a,
+                                         __amdgpu_buffer_rsrc_t rmain, int t, int tbl, int rowb,
+                                         int lane, const bool (&on)[NV]) {
+  const int off = t * rowb + lane * 16;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    o[v] = on[v] ? bload4<0>(rmain, off + 1024 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
+  if (t < a.stripe_rows) {
+    const float* sb = a.stripe + (int64_t)tbl * (a.stripe_copies - 1) * a.stripe_rows * a.ld;
+    for (int c = 1; c < a.stripe_copies; ++c) {
+      const float4* sr = reinterpret_cast<const float4*>(
+          sb + ((int64_t)(c - 1) * a.stripe_rows + t) * a.ld);
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        if (!on[v]) continue;
+        const float4 q = sr[lane + 64 * v];
+        o[v].x += q.x;
+        o[v].y += q.y;
+        o[v].z += q.z;
+        o[v].w += q.w;
+      }
+    }
+  }
+}
+
+// destination of an atomic delta for row t of table tbl: main or stripe copy c
+__device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int c) {
+  if (c == 0 || t >= a.stripe_rows) return (tbl ? a.wr1 : a.wr0) + (int64_t)t * a.ld;
+  return a.stripe + (((int64_t)tbl * (a.stripe_copies - 1) + (c - 1)) * a.stripe_rows + t) * a.ld;
+}
+
 template <int K, int NV>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a, int64_t e,
                                              __amdgpu_buffer_rsrc_t r0,
@@ -592,17 +626,15 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
 #pragma unroll
   for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
-  const int in_off = x.input * rowb + lane * 16;
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-    x.l1[v] = on[v] ? bload4<0>(r0, in_off + 1024 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
+  load_row<NV>(x.l1, a, r0, x.input, 0, rowb, lane, on);
 #pragma unroll
   for (int d = 0; d <= K; ++d) {
-    const int off = (x.tg[d] < 0 ? 0 : x.tg[d]) * rowb + lane * 16;
+    if (x.tg[d] >= 0) {
+      load_row<NV>(x.rw[d], a, r1, x.tg[d], 1, rowb, lane, on);
+    } else {
 #pragma unroll
-    for (int v = 0; v < NV; ++v)
-      x.rw[d][v] = (on[v] && x.tg[d] >= 0) ? bload4<0>(r1, off + 1024 * v)
-                                           : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
   }
 }
 
@@ -637,8 +669,6 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.rd0, tbytes);
   const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.rd1, tbytes);
   const int rowb = (int)a.ld * 4;
-  float* S0 = a.wr0;
-  float* S1 = a.wr1;
   float* s1 = s_l1[wid];
   float* sw = s_wk[wid];
   bool on[NV];
@@ -725,14 +755,15 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       if (e + 1 < e_end) load_example<K, NV>(x, a, e + 1, r0, r1, rowb, lane, on);
 
       // ---- atomics of example e -----------------------------------------------
+      const int cbase = (int)(e % (int64_t)a.stripe_copies);
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         if (g[d] == 0.f) continue;
-        float* row = S1 + (int64_t)tg[d] * a.ld + lane;
+        float* row = upd_row(a, 1, tg[d], (cbase + d) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, g[d] * s1[64 * i + lane]);
       }
       if (any) {
-        float* row = S0 + (int64_t)input * a.ld + lane;
+        float* row = upd_row(a, 0, input, (cbase + NT) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, lf * sw[64 * i + lane]);
       }
       if (tail) {
@@ -741,23 +772,23 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           const int q = q0 + lane / tail;
           const int el = full * 64 + lane % tail;
           float coef = 0.f;
-          int64_t base = 0;
-          bool from_work = false;
+          int row_t = 0;
 #pragma unroll
           for (int d = 0; d < NT; ++d) {
             if (q == d) {
               coef = g[d];
-              base = (int64_t)(tg[d] < 0 ? 0 : tg[d]) * a.ld;
+              row_t = tg[d] < 0 ? 0 : tg[d];
             }
           }
-          if (q == NT) {
+          const bool from_work = (q == NT);
+          if (from_work) {
             coef = any ? lf : 0.f;
-            base = (int64_t)input * a.ld;
-            from_work = true;
+            row_t = input;
           }
           if (lane / tail < tpack && q <= NT && coef != 0.f) {
             const float src = from_work ? sw[el] : s1[el];
-            upd<WR>((from_work ? S0 : S1) + base + el, coef * src);
+            float* row = upd_row(a, from_work ? 0 : 1, row_t, (cbase + q) % a.stripe_copies);
+            upd<WR>(row + el, coef * src);
           }
         }
       }
@@ -925,6 +956,37 @@ int sgns_blocks_per_cu(int K, int nv) {
 #undef G2V_OCC
   if (e != hipSuccess || nb <= 0) nb = 1;
   return nb;
+}
+
+
+// fold the stripe copies of the hot rows into the main rows, zero the copies
+__global__ void k_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
+                               int64_t ld, int nvec) {
+  const int t = blockIdx.x;      // hot row
+  const int tbl = blockIdx.y;    // 0 syn0, 1 syn1neg
+  const int col = threadIdx.x;   // float4 column
+  if (col >= nvec) return;
+  float4* m = reinterpret_cast<float4*>((tbl ? syn1 : syn0) + (int64_t)t * ld) + col;
+  float4 acc = *m;
+  for (int c = 1; c < copies; ++c) {
+    float4* p = reinterpret_cast<float4*>(
+                    stripe + (((int64_t)tbl * (copies - 1) + (c - 1)) * rows + t) * ld) + col;
+    const float4 q = *p;
+    acc.x += q.x;
+    acc.y += q.y;
+    acc.z += q.z;
+    acc.w += q.w;
+    *p = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  *m = acc;
+}
+
+hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
+                               int64_t ld, int nvec, hipStream_t st) {
+  if (rows <= 0 || copies <= 1) return hipSuccess;
+  hipLaunchKernelGGL(k_fold_stripes, dim3(rows, 2), dim3(128), 0, st, syn0, syn1, stripe, rows,
+                     copies, ld, nvec);
+  return hipGetLastError();
 }
 
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,

@@ -99,13 +99,18 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
  *                         2 uncached (re-allocates, zero-filled) [0]
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
- *                         atomics, 2 no table writes [0] */
+ *                         atomics, 2 no table writes [0]
+ *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
+ *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off [8] (values stay exact:
+ *                         readers sum the copies, each launch folds them back) */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
 #define G2V_OPT_GRID 4
 #define G2V_OPT_TABLE_MEM 5
 #define G2V_OPT_DEBUG_WRITE 6
+#define G2V_OPT_STRIPE_ROWS 7
+#define G2V_OPT_STRIPE_COPIES 8
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);

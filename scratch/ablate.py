@@ -10,11 +10,11 @@ V = len(order); vc = counts[order]; tok = remap[flat]
 js = E.plan_jobs(n_sent=NP, sent_len=2); al = E.job_alphas(js, NP)
 rng = np.random.Generator(np.random.PCG64(1)); syn0 = ((rng.random((V, D)) - 0.5) / D).astype(np.float32)
 for spec in sys.argv[1].split(","):
-    wr, grid = map(int, spec.split(":"))
+    wr, grid, H, R = (list(map(int, spec.split(":"))) + [64, 4])[:4]
     eng = E.SGNSEngine(V, D, K); eng.set_vocab(vc, 1e-3); eng.set_corpus(tok, sent_len=2)
-    eng.set_weights(syn0, np.zeros((V, D), np.float32)); eng.set_option(N.OPT_DEBUG_WRITE, wr); eng.set_option(N.OPT_GRID, grid)
+    eng.set_weights(syn0, np.zeros((V, D), np.float32)); eng.set_option(N.OPT_DEBUG_WRITE, wr); eng.set_option(N.OPT_GRID, grid); eng.set_option(N.OPT_STRIPE_ROWS, H); eng.set_option(N.OPT_STRIPE_COPIES, R)
     rs = np.random.RandomState(1)
     for it in range(2):
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD, timing=True); st = eng.read_stats()
-    print("write", wr, "grid", grid, "ex/s %.3g" % (st["examples"] / st["sgns_kernel_ms"] * 1e3), "launch ms %.2f" % (st["sgns_kernel_ms"] / st["launches"]), flush=True)
+    print("write", wr, "grid", grid, "H", H, "R", R, "ex/s %.3g" % (st["examples"] / st["sgns_kernel_ms"] * 1e3), "launch ms %.2f" % (st["sgns_kernel_ms"] / st["launches"]), flush=True)
     eng.close()
