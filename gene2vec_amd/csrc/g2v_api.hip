@@ -798,6 +798,34 @@ int g2v_sgns_step_explicit(g2v_ctx* c, const int32_t* center, const int32_t* inp
   return G2V_OK;
 }
 
+int g2v_cosine_pairs(int device, const float* vectors, int64_t V, int32_t D, const int32_t* a,
+                     const int32_t* b, int64_t n, float* out) {
+  REQUIRE(vectors && (n == 0 || (a && b && out)), G2V_EINVAL, "null argument");
+  REQUIRE(V > 0 && D > 0 && n >= 0, G2V_EINVAL, "bad sizes");
+  for (int64_t i = 0; i < n; ++i)
+    REQUIRE(a[i] >= 0 && a[i] < V && b[i] >= 0 && b[i] < V, G2V_EINVAL,
+            "pair %lld index out of range", (long long)i);
+  HIPCHK(hipSetDevice(device));
+  float *dv = nullptr, *du = nullptr, *dout = nullptr;
+  int32_t* dab = nullptr;
+  int rc = G2V_OK;
+  const size_t tab = (size_t)V * (size_t)D;
+  if ((rc = dev_alloc(&dv, tab)) || (rc = dev_alloc(&du, tab)) ||
+      (rc = dev_alloc(&dab, 2 * (size_t)n)) || (rc = dev_alloc(&dout, (size_t)n))) {
+    dev_free(dv); dev_free(du); dev_free(dab); dev_free(dout);
+    return rc;
+  }
+  hipError_t e = hipMemcpy(dv, vectors, tab * sizeof(float), hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(dab, a, n * sizeof(int32_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess && n) e = hipMemcpy(dab + n, b, n * sizeof(int32_t), hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = launch_cosine_pairs(dv, V, D, du, dab, dab + n, n, dout, nullptr);
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess && n) e = hipMemcpy(out, dout, n * sizeof(float), hipMemcpyDeviceToHost);
+  dev_free(dv); dev_free(du); dev_free(dab); dev_free(dout);
+  if (e != hipSuccess) return fail(G2V_EHIP, "g2v_cosine_pairs: %s", hipGetErrorString(e));
+  return G2V_OK;
+}
+
 int g2v_sync(g2v_ctx* c) {
   int rc = set_dev(c);
   if (rc) return rc;

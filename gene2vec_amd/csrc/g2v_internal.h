@@ -95,6 +95,8 @@ hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int pol, int 
 int sgns_blocks_per_cu(int K, int nv);
 hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
                                int64_t ld, int nvec, hipStream_t st);
+hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const int32_t* a,
+                               const int32_t* b, int64_t n, float* out, hipStream_t st);
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
                         double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
                         hipStream_t st);

@@ -1000,3 +1000,49 @@ hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double p
 }
 
 }  // namespace g2v
+
+// ---------------------------------------------------------------------------
+// consumer-side: word similarities for the manuscript target function
+// (src/evaluation_target_function.py:38,49 -> gensim wv.similarity =
+// dot(unitvec(a), unitvec(b)), unitvec = sscal(1/snrm2(v), v) in float32)
+// ---------------------------------------------------------------------------
+namespace g2v {
+
+// one wave per row: unit[r] = v[r] * (float)(1 / (float)||v[r]||)
+__global__ void k_unitvec(const float* __restrict__ v, int64_t V, int D, float* __restrict__ u) {
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= V) return;
+  const float* row = v + r * D;
+  double s = 0.0;
+  for (int k = lane; k < D; k += 64) s = fma((double)row[k], (double)row[k], s);
+  s = wave_allreduce_d(s);
+  const float len = (float)sqrt(s);
+  const float inv = len > 0.f ? (float)(1.0 / (double)len) : 1.f;
+  for (int k = lane; k < D; k += 64) u[r * D + k] = row[k] * inv;
+}
+
+// one wave per pair: out[i] = (float) dot(u[a[i]], u[b[i]])
+__global__ void k_pair_dot(const float* __restrict__ u, int D, const int32_t* __restrict__ a,
+                           const int32_t* __restrict__ b, int64_t n, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= n) return;
+  const float* x = u + (int64_t)a[i] * D;
+  const float* y = u + (int64_t)b[i] * D;
+  double s = 0.0;
+  for (int k = lane; k < D; k += 64) s = fma((double)x[k], (double)y[k], s);
+  s = wave_allreduce_d(s);
+  if (lane == 0) out[i] = (float)s;
+}
+
+hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const int32_t* a,
+                               const int32_t* b, int64_t n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_unitvec, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, v, V, D, u);
+  if (n > 0)
+    hipLaunchKernelGGL(k_pair_dot, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, u, D, a, b, n,
+                       out);
+  return hipGetLastError();
+}
+
+}  // namespace g2v

@@ -182,6 +182,14 @@ int g2v_sync(g2v_ctx *ctx);
 /* Accumulated since the previous call (synchronises, then resets). */
 int g2v_read_stats(g2v_ctx *ctx, g2v_stats *out);
 
+/* ---- consumer side ----------------------------------------------------------------- */
+/* gensim wv.similarity for n index pairs (src/evaluation_target_function.py:38,49):
+ * out[i] = dot(unitvec(v[a[i]]), unitvec(v[b[i]])), unitvec = v * (1/||v||) in
+ * float32, dots accumulated in double and rounded to float.  vectors: host
+ * [V][D] fp32.  Standalone (own device buffers), synchronises. */
+int g2v_cosine_pairs(int device, const float *vectors, int64_t V, int32_t D, const int32_t *a,
+                     const int32_t *b, int64_t n, float *out);
+
 /* ---- host-native helpers (no device work) -------------------------------------- */
 /* [ext] Word2VecTrainables.seeded_vector for every row: row i =
  * (RandomState(seeds[i]).rand(D) - 0.5) / D as float32, seeds[i] =
