@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libg2v.so")
-SOURCES = ["g2v_kernels.hip", "g2v_api.hip", "g2v_host.cpp"]
+SOURCES = ["g2v_kernels.hip", "g2v_api.hip", "g2v_host.cpp", "g2v_ingest.cpp"]
 HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(ROOT, "include", "g2v.h")]
 ARCH = "gfx950"
 
@@ -42,7 +42,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     tmp = LIB + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            # IEEE semantics: every fused multiply-add in the kernels is explicit
-           "-ffp-contract=off", "-munsafe-fp-atomics",
+           "-ffp-contract=off", "-munsafe-fp-atomics", "-pthread",
            "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

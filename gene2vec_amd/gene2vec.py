@@ -24,6 +24,7 @@ import random
 import zlib
 
 from . import generateMatrix as gM
+from . import ingest
 from .word2vec import Word2Vec
 
 
@@ -54,6 +55,14 @@ def _hashfxn(name):
     raise ValueError(name)
 
 
+def _vocab_ids(model, corpus):
+    """corpus word id -> model vocabulary index (-1 when not in the vocabulary)"""
+    import numpy as np
+    voc = model.wv.vocab
+    return np.array([voc[w].index if w in voc else -1 for w in corpus.words] or [0],
+                    dtype=np.int32)
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(
         description="Please specify data directory, embedding output directory and data file "
@@ -72,6 +81,9 @@ def main(argv=None):
                         help="seed Python's shuffles (the reference leaves them unseeded)")
     parser.add_argument("--hash", choices=("python", "crc32"), default="python",
                         help="seeded_vector hash (gensim default: Python's randomised hash)")
+    parser.add_argument("--native-ingest", action="store_true",
+                        help="multi-threaded C++ reader + bit-compatible native shuffles "
+                             "(same result as the Python ingest for the same seed)")
     parser.add_argument("--no-txt", action="store_true")
     parser.add_argument("--no-w2v", action="store_true")
     parser.add_argument("--w2v-binary", action="store_true")
@@ -81,35 +93,66 @@ def main(argv=None):
     logging.basicConfig(format="%(asctime)s : %(levelname)s : %(message)s", level=logging.INFO)
     print("start!")
     rng = random.Random(args.shuffle_seed) if args.shuffle_seed is not None else random
-    gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
+    corpus = None
+    if args.native_ingest:
+        files = os.listdir(source_dir)
+        rng.shuffle(files)
+        paths = [os.path.join(source_dir, f) for f in files if f.endswith(ending_pattern)]
+        print(datetime.datetime.now())
+        print(f"native ingest of {len(paths)} files")
+        corpus = ingest.read_corpus(paths)
+        n_pairs = corpus.n_sent
+    else:
+        gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
+        n_pairs = len(gene_pairs)
     print(datetime.datetime.now())
-    print("shuffle start " + str(len(gene_pairs)))
-    rng.shuffle(gene_pairs)
+    print("shuffle start " + str(n_pairs))
+    if corpus is not None:
+        corpus = corpus.permuted(ingest.py_shuffle_perm(corpus.n_sent, rng))
+    else:
+        rng.shuffle(gene_pairs)
     print(datetime.datetime.now())
-    print("shuffle done " + str(len(gene_pairs)))
+    print("shuffle done " + str(n_pairs))
 
     dimension = args.dim
     hashfxn = _hashfxn(args.hash)
     os.makedirs(export_dir, exist_ok=True)
     outputs = []
+    kw = dict(size=dimension, window=args.window, min_count=1, workers=args.workers, iter=1, sg=1,
+              negative=args.negative, sample=args.sample, hashfxn=hashfxn, device=args.device,
+              mode=args.mode)
     for current_iter in range(1, args.iters + 1):
         name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
         if current_iter == 1:
             print(f"gene2vec dimension {dimension} iteration {current_iter} start")
-            model = Word2Vec(gene_pairs, size=dimension, window=args.window, min_count=1,
-                             workers=args.workers, iter=1, sg=1, negative=args.negative,
-                             sample=args.sample, hashfxn=hashfxn, device=args.device,
-                             mode=args.mode)
+            if corpus is None:
+                model = Word2Vec(gene_pairs, **kw)
+            else:
+                model = Word2Vec(**kw)
+                model._build_from_counts(corpus.vocab_raw_counts())
+                model.corpus_count = corpus.n_sent
+                model.corpus_total_words = int(corpus.sent_off[-1])
+                ids = _vocab_ids(model, corpus)
+                model.train_ids(ids[corpus.tokens], corpus.sent_off,
+                                total_examples=model.corpus_count, epochs=model.iter)
         else:
             print(datetime.datetime.now())
-            print("shuffle start " + str(len(gene_pairs)))
-            rng.shuffle(gene_pairs)
+            print("shuffle start " + str(n_pairs))
+            if corpus is not None:
+                corpus = corpus.permuted(ingest.py_shuffle_perm(corpus.n_sent, rng))
+            else:
+                rng.shuffle(gene_pairs)
             print(datetime.datetime.now())
-            print("shuffle done " + str(len(gene_pairs)))
+            print("shuffle done " + str(n_pairs))
             print(f"gene2vec dimension {dimension} iteration {current_iter} start")
             prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
             model = Word2Vec.load(prev, device=args.device)
-            model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
+            if corpus is None:
+                model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
+            else:
+                ids = _vocab_ids(model, corpus)
+                model.train_ids(ids[corpus.tokens], corpus.sent_off,
+                                total_examples=model.corpus_count, epochs=model.iter)
         model.save(name)
         if not args.no_txt:
             gM.outputTxt(name)

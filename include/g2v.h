@@ -200,6 +200,25 @@ int g2v_seeded_vectors(const uint32_t *seeds, int64_t n_rows, int32_t dim, float
  * [0, V) over ids[n]; the vocabulary scan of [ext] scan_vocab on pre-hashed ids. */
 int g2v_count_ids(const int32_t *ids, int64_t n, int32_t V, int64_t *counts, int64_t *first);
 
+/* ---- native ingest (src/gene2vec.py:36-47 and the shuffles at :52/:80) ----------- */
+/* Reads files in the given order as windows-1252 text: universal newlines,
+ * str.split() separators (ASCII whitespace, 0x1c-0x1f, 0xa0); every line is one
+ * sentence (empty lines included).  Token ids follow global first occurrence.
+ * Undefined windows-1252 bytes -> G2V_EINVAL (UnicodeDecodeError upstream). */
+typedef struct g2v_corpus g2v_corpus;
+int g2v_corpus_read(const char *const *paths, int n_paths, int n_threads, g2v_corpus **out);
+int g2v_corpus_info(const g2v_corpus *c, int64_t *n_tokens, int64_t *n_sent, int64_t *n_words,
+                    int64_t *word_bytes);
+int g2v_corpus_export(const g2v_corpus *c, int32_t *tokens, int64_t *sent_off, int64_t *counts,
+                      char *words, int64_t *word_off);
+int g2v_corpus_free(g2v_corpus *c);
+/* out sentence i = in sentence perm[i] (CSR gather) */
+int g2v_csr_permute(const int32_t *tok, const int64_t *off, int64_t n_sent, const int64_t *perm,
+                    int32_t *out_tok, int64_t *out_off);
+/* CPython random.Random.shuffle(x) bit for bit; state624/pos = getstate()[1][:625],
+ * updated in place (setstate afterwards keeps Python's generator in step). */
+int g2v_py_shuffle(uint32_t *state624, uint32_t *pos, int64_t *x, int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

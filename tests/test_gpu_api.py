@@ -80,3 +80,21 @@ def test_cli_end_to_end_matches_oracle(tmp_path, test_pairs):
     got = np.array([r[1:] for r in rows], dtype=np.float32)
     np.testing.assert_allclose(got, syn0[[voc.word2index[w] for w in voc.first_order]],
                                rtol=1e-5, atol=1e-7)
+
+
+def test_cli_native_ingest_equals_python_ingest(tmp_path):
+    data = tmp_path / "data"
+    data.mkdir()
+    rng = np.random.RandomState(3)
+    genes = [f"G{i}" for i in range(400)]
+    for k in range(3):
+        lines = [f"{genes[a]} {genes[b]}" for a, b in rng.randint(0, 400, (3000, 2)) if a != b]
+        (data / f"s{k}.txt").write_text("\n".join(lines) + ("\n" if k else ""))
+    outs = {}
+    for tag, extra in (("py", []), ("native", ["--native-ingest"])):
+        out = tmp_path / tag
+        cli_main([str(data), str(out), "txt", "--iters", "2", "--dim", "64", "--mode",
+                  "sequential", "--hash", "crc32", "--shuffle-seed", "11", "--no-txt"] + extra)
+        outs[tag] = KeyedVectors.load_word2vec_format(str(out / "gene2vec_dim_64_iter_2_w2v.txt"))
+    assert outs["py"].index2word == outs["native"].index2word
+    np.testing.assert_array_equal(outs["py"].vectors, outs["native"].vectors)

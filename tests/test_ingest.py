@@ -1,0 +1,93 @@
+"""Native ingest == the reference's Python ingest (src/gene2vec.py:36-52)."""
+import random
+
+import numpy as np
+import pytest
+
+from gene2vec_amd.ingest import py_shuffle_perm, read_corpus
+
+
+def _py_read(paths):
+    out = []
+    for p in paths:
+        with open(p, "r", encoding="windows-1252") as f:
+            for line in f:
+                out.append(line.strip().split())
+    return out
+
+
+@pytest.fixture
+def files(tmp_path):
+    rng = np.random.RandomState(0)
+    genes = ["TP53", "G\xe9ne", "ABC-1", "X", "hla_a"] + [f"G{i}" for i in range(300)]
+    seps = [" ", "\t", "  ", "\xa0", "\x1c", " \x0b "]
+    ends = ["\n", "\r\n", "\r"]
+    paths = []
+    for k in range(3):
+        lines = []
+        for _ in range(2000):
+            n = rng.choice([0, 1, 2, 2, 2, 4])
+            toks = [genes[int(i)] for i in rng.randint(0, len(genes), n)]
+            sep = seps[rng.randint(len(seps))]
+            lines.append((" " if rng.rand() < 0.1 else "") + sep.join(toks) +
+                         ends[rng.randint(len(ends))])
+        text = "".join(lines)
+        if k == 1:
+            text = text.rstrip("\r\n")  # no trailing newline
+        p = tmp_path / f"f{k}.txt"
+        p.write_bytes(text.encode("windows-1252"))
+        paths.append(str(p))
+    (tmp_path / "empty.txt").write_bytes(b"")
+    paths.append(str(tmp_path / "empty.txt"))
+    return paths
+
+
+def test_native_reader_matches_python(files):
+    ref = _py_read(files)
+    for threads in (1, 4):
+        c = read_corpus(files, threads=threads)
+        assert c.n_sent == len(ref)
+        assert c.sentences() == ref
+        words_fo = []
+        seen = set()
+        for s in ref:
+            for w in s:
+                if w not in seen:
+                    seen.add(w)
+                    words_fo.append(w)
+        assert c.words == words_fo
+        assert int(c.counts.sum()) == sum(len(s) for s in ref)
+
+
+def test_undefined_cp1252_byte_raises(tmp_path):
+    p = tmp_path / "bad.txt"
+    p.write_bytes(b"A B\nC \x81D\n")
+    with pytest.raises(UnicodeDecodeError):
+        open(p, encoding="windows-1252").read()
+    with pytest.raises(UnicodeDecodeError):
+        read_corpus([str(p)])
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 10, 1000, 123457])
+def test_py_shuffle_perm_bit_compatible(n):
+    r1, r2 = random.Random(12345), random.Random(12345)
+    data = list(range(n))
+    r1.shuffle(data)
+    perm = py_shuffle_perm(n, r2)
+    assert perm.tolist() == data
+    assert r1.getstate() == r2.getstate()
+    assert r1.random() == r2.random()
+
+
+def test_permuted_corpus_and_vocab(files):
+    ref = _py_read(files)
+    c = read_corpus(files)
+    r1, r2 = random.Random(7), random.Random(7)
+    r1.shuffle(ref)
+    c2 = c.permuted(py_shuffle_perm(c.n_sent, r2))
+    assert c2.sentences() == ref
+    raw = {}
+    for s in ref:
+        for w in s:
+            raw[w] = raw.get(w, 0) + 1
+    assert list(c2.vocab_raw_counts().items()) == list(raw.items())
