@@ -49,7 +49,9 @@ def parse():
     p.add_argument("--negative", type=int, default=5)
     p.add_argument("--sample", type=float, default=1e-3)
     p.add_argument("--zipf", type=float, default=1.0)
-    p.add_argument("--avg-every-jobs", type=int, default=5000, help="RCCL averaging cadence (N>1)")
+    p.add_argument("--avg-every-jobs", type=int, default=1024, help="RCCL merge cadence (N>1)")
+    p.add_argument("--merge", choices=("touch", "mean"), default="touch",
+                   help="replica merge rule (gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
     p.add_argument("--cpu-threads", type=int, default=0)
@@ -127,7 +129,7 @@ def main():
     rs = np.random.RandomState(Dd.rank_seed(1, rank))  # gensim model.random(seed=1) per rank
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
-    trainer = Dd.ReplicaTrainer(eng, (syn0, syn1), avg_every, N.MODE_HOGWILD)
+    trainer = Dd.ReplicaTrainer(eng, (syn0, syn1), avg_every, N.MODE_HOGWILD, merge=a.merge)
     torch.cuda.synchronize(dev)
 
     def step(i, timing):
@@ -241,11 +243,11 @@ def main():
                 "workload": ("C2: synthetic Zipf(1.0) gene pairs, V=24447, 100M pairs, dim 200, "
                              "neg 5, window 1, sample 1e-3, 1 epoch per step") if world == 1 else
                             (f"C3: synthetic Zipf gene pairs, V=24447, {n_pairs} pairs per GPU x "
-                             f"{world}, dim 200, neg 5, RCCL model averaging every "
-                             f"{avg_every} jobs"),
+                             f"{world}, dim 200, neg 5, RCCL row-wise replica merge ({a.merge}) "
+                             f"every {avg_every} jobs"),
                 "vocab": V, "pairs_per_gpu": n_pairs, "dim": D, "negative": K,
                 "sample": a.sample, "window": 1,
-                "parallelism": f"dp{world}" + (" + RCCL AVG all-reduce" if world > 1 else "")},
+                "parallelism": f"dp{world}" + (f" + RCCL all-reduce {a.merge} merge" if world > 1 else "")},
             "examples_per_s": round(total_examples / elapsed, 1),
             "effective_examples": total_examples,
             "roofline": roofline, "cpu_baseline": cpu, "quality": quality,

@@ -72,19 +72,48 @@ def average_(tensors, group=None):
         t.mul_(1.0 / world)
 
 
+def touch_merge_(tensors, olds, beta=1.0, group=None):
+    """Row-wise replica merge: new = old + sum_r(d_r) / k**beta, d_r = replica r's
+    change since the last merge, k = number of replicas whose row changed.
+
+    A row only one replica trained keeps that replica's full update (plain
+    averaging would divide it by N); a row every replica trained gets the
+    mean of their updates (summing would overshoot the hot rows -- measured:
+    summed deltas diverge).  ``olds`` hold the tables at the last merge and
+    are updated in place."""
+    import torch
+    import torch.distributed as dist
+    single = not dist.is_initialized() or dist.get_world_size(group) == 1
+    for t, old in zip(tensors, olds):
+        d = t - old
+        cnt = (d != 0).any(dim=1).to(t.dtype)
+        if not single:
+            dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
+            dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
+        k = torch.clamp(cnt, min=1.0)
+        if beta != 1.0:
+            k = k ** beta
+        t.copy_(old + d / k[:, None])
+        old.copy_(t)
+
+
 class ReplicaTrainer:
     """Drives one rank: trains job windows on an engine-like object and
-    averages the replicas between windows.
+    merges the replicas between windows.
 
     engine: has ``train(job_sent, alpha, seed, mode, timing=...)``.
-    tables: the torch tensors bound into the engine (averaged in place).
+    tables: the torch tensors bound into the engine (merged in place).
+    merge:  "touch" (row-wise, default) or "mean" (plain model averaging).
     """
 
-    def __init__(self, engine, tables, avg_every_jobs, mode=0):
+    def __init__(self, engine, tables, avg_every_jobs, mode=0, merge="touch", beta=1.0):
         self.engine = engine
         self.tables = list(tables)
         self.avg_every_jobs = max(1, int(avg_every_jobs))
         self.mode = mode
+        self.merge = merge
+        self.beta = beta
+        self.olds = [t.clone() for t in self.tables] if merge == "touch" else None
         self.averages = 0
 
     def train_epoch(self, job_sent, alphas, seeds, timing=False):
@@ -93,5 +122,11 @@ class ReplicaTrainer:
             j1 = min(n_jobs, j0 + self.avg_every_jobs)
             self.engine.train(job_sent[j0:j1 + 1], alphas[j0:j1], seeds[j0:j1], self.mode,
                               timing=timing)
+            self.sync_replicas()
+
+    def sync_replicas(self):
+        if self.merge == "touch":
+            touch_merge_(self.tables, self.olds, self.beta)
+        else:
             average_(self.tables)
-            self.averages += 1
+        self.averages += 1

@@ -54,12 +54,20 @@ def _worker(rank, world, port, q):
         # cadence: 10 jobs, average every 4 -> windows of 4, 4, 2
         tabs = [torch.zeros(2, 2), torch.zeros(3)]
         eng = FakeEngine(tabs, rank)
-        tr = Dd.ReplicaTrainer(eng, tabs, avg_every_jobs=4)
+        tr = Dd.ReplicaTrainer(eng, tabs, avg_every_jobs=4, merge="mean")
         js = np.arange(0, 21, 2, dtype=np.int64)
         tr.train_epoch(js, np.zeros(10), np.zeros(10, np.uint64))
         out["calls"] = eng.calls
         out["tables"] = [x.numpy() for x in tabs]
         out["averages"] = tr.averages
+        # row-wise touch merge: rank 0 changes rows {0, 1}, rank 1 rows {1, 2}
+        t = torch.zeros(4, 3)
+        olds = [t.clone()]
+        rows = [0, 1] if rank == 0 else [1, 2]
+        t[rows] += float(rank + 1)
+        Dd.touch_merge_([t], olds)
+        out["touch"] = t.numpy()
+        out["touch_old"] = olds[0].numpy()
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -110,3 +118,13 @@ def test_replica_trainer_cadence_and_consistency(results):
     for t0, t1 in zip(results[0]["tables"], results[1]["tables"]):
         assert np.array_equal(t0, t1)
         assert np.allclose(t0, 15.0)
+
+
+def test_touch_merge_rowwise(results):
+    for r in (0, 1):
+        t = results[r]["touch"]
+        assert np.allclose(t[0], 1.0)        # only rank 0: full update kept
+        assert np.allclose(t[1], 1.5)        # both ranks: mean of (1, 2)
+        assert np.allclose(t[2], 2.0)        # only rank 1
+        assert np.allclose(t[3], 0.0)        # untouched
+        assert np.array_equal(results[r]["touch_old"], t)
