@@ -98,3 +98,24 @@ def test_cli_native_ingest_equals_python_ingest(tmp_path):
         outs[tag] = KeyedVectors.load_word2vec_format(str(out / "gene2vec_dim_64_iter_2_w2v.txt"))
     assert outs["py"].index2word == outs["native"].index2word
     np.testing.assert_array_equal(outs["py"].vectors, outs["native"].vectors)
+
+
+def test_ggipnn_auc_parity_gpu_vs_oracle(tmp_path):
+    """End-to-end on the reference's own labelled data (data/predictionData):
+    gene2vec embeddings from the GPU engine (Hogwild) vs the sequential
+    oracle, scored by the GGIPNN classifier; north star: within 1 %."""
+    import importlib.util
+    import os as _os
+    spec = importlib.util.spec_from_file_location(
+        "ggipnn_e2e", _os.path.join(_os.path.dirname(GOLDEN), "..", "scripts", "ggipnn_e2e.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    m.train("gpu", str(tmp_path / "g"), 4, 7)
+    m.train("oracle", str(tmp_path / "o"), 4, 7)
+    from gene2vec_amd import ggipnn as G
+    ag = np.mean([G.train_and_auc(str(tmp_path / "g" / "emb.txt"), m.DATA, seed=s, device="cuda")
+                  for s in (0, 1)])
+    ao = np.mean([G.train_and_auc(str(tmp_path / "o" / "emb.txt"), m.DATA, seed=s, device="cuda")
+                  for s in (0, 1)])
+    assert ao > 0.9
+    assert abs(ag - ao) / ao < 0.01, (ag, ao)
