@@ -15,8 +15,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libg2v.so")
-SOURCES = ["g2v_kernels.hip", "g2v_api.hip", "g2v_host.cpp", "g2v_ingest.cpp"]
-HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(ROOT, "include", "g2v.h")]
+K_COMPILED = (1, 2, 3, 5, 10, 15, 20)  # == G2V_FOR_EACH_K in g2v_internal.h
+# (source, extra defines, object name): the SGNS kernels are built once per K
+UNITS = ([("g2v_sgns_atomic.hip", [f"-DG2V_K={k}"], f"g2v_sgns_atomic_k{k}.o") for k in K_COMPILED]
+         + [("g2v_sgns.hip", [f"-DG2V_K={k}"], f"g2v_sgns_k{k}.o") for k in K_COMPILED]
+         + [(s, [], os.path.splitext(s)[0] + ".o")
+            for s in ("g2v_kernels.hip", "g2v_api.hip", "g2v_host.cpp", "g2v_ingest.cpp")])
+SOURCES = sorted({u[0] for u in UNITS})
+HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(CSRC, "g2v_device.h"),
+           os.path.join(ROOT, "include", "g2v.h")]
 ARCH = "gfx950"
 
 
@@ -36,14 +43,39 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile every translation unit in parallel (one hipcc per file), then link."""
     if not force and not _stale():
         return LIB
-    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(HERE, "build")
+    os.makedirs(objdir, exist_ok=True)
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+             # IEEE semantics: every fused multiply-add in the kernels is explicit
+             "-ffp-contract=off", "-munsafe-fp-atomics", "-pthread",
+             "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    objs = [os.path.join(objdir, u[2]) for u in UNITS]
+
+    def compile_one(i):
+        src, defs, _ = UNITS[i]
+        deps = [os.path.join(CSRC, src)] + HEADERS + [__file__]
+        if (not force and os.path.exists(objs[i])
+                and all(os.path.getmtime(d) <= os.path.getmtime(objs[i]) for d in deps)):
+            return ""
+        cmd = [hipcc(), *flags, *defs, "-c", os.path.join(CSRC, src), "-o", objs[i]]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError(f"hipcc failed on {src} {defs}:\n{r.stderr}")
+        return r.stderr
+
+    jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(UNITS), os.cpu_count() or 1, 16)
+    with ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
+        for err in ex.map(compile_one, range(len(UNITS))):
+            if err and verbose:
+                print(err, file=sys.stderr)
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           # IEEE semantics: every fused multiply-add in the kernels is explicit
-           "-ffp-contract=off", "-munsafe-fp-atomics", "-pthread",
-           "-I", os.path.join(ROOT, "include"), "-I", CSRC, *srcs, "-o", tmp]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

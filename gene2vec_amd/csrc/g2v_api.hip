@@ -627,21 +627,20 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.hot_rows = c->hot_rows < 0 ? c->V : std::min(c->hot_rows, c->V);
   s.exp_table = c->exp_table;
   s.debug_write = c->debug_write;
-  const bool striped = mode == kModeHogwild && s.hot_rows >= c->V && c->stripe_copies > 1 &&
-                       c->stripe_rows > 0;
+  const bool atomic_kernel = mode == kModeHogwild && s.hot_rows >= c->V;
+  const bool striped = atomic_kernel && c->stripe_copies > 1 && c->stripe_rows > 0;
   s.stripe_rows = striped ? std::min(c->stripe_rows, c->V) : 0;
   s.stripe_copies = striped ? c->stripe_copies : 1;
+  int rc;
   if (striped) {
     const int64_t need = 2 * (int64_t)(s.stripe_copies - 1) * s.stripe_rows * c->ld;
     if (need > c->stripe_cap) {
-      int rc2 = dev_reserve(c->stream, &c->stripe, &c->stripe_cap, need);
-      if (rc2) return rc2;
+      if ((rc = dev_reserve(c->stream, &c->stripe, &c->stripe_cap, need))) return rc;
       HIPCHK(hipMemsetAsync(c->stripe, 0, sizeof(float) * c->stripe_cap, c->stream));
     }
   }
   s.stripe = c->stripe;
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  int rc;
   if (timing) {
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
     HIPCHK(hipEventRecord(e0, c->stream));

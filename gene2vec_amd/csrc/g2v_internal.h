@@ -89,9 +89,20 @@ hipError_t launch_scan_jobs(const int32_t* nex, int64_t nj, int64_t* off,
 hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
                                    const int32_t* negs, int64_t n, int K, float alpha,
                                    int rec_stride, int32_t* rec, hipStream_t st);
+// negative counts compiled into the SGNS kernels; g2v_sgns.hip and
+// g2v_sgns_atomic.hip are built once per K (-DG2V_K=K) and define the per-K
+// entry points below; the dispatchers live in g2v_kernels.hip
+#define G2V_FOR_EACH_K(X) X(1) X(2) X(3) X(5) X(10) X(15) X(20)
+#define G2V_DECL_K(KK)                                                                     \
+  hipError_t launch_sgns_k##KK(const SgnsArgs& a, int nv, int mode, int pol, int grid,     \
+                               hipStream_t st);                                            \
+  hipError_t launch_sgns_atomic_k##KK(const SgnsArgs& a, int nv, int grid, hipStream_t st); \
+  int sgns_blocks_per_cu_k##KK(int nv);
+G2V_FOR_EACH_K(G2V_DECL_K)
 bool sgns_supported(int K, int nv);
 hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int pol, int grid,
                        hipStream_t st);
+hipError_t launch_sgns_atomic(const SgnsArgs& a, int K, int nv, int grid, hipStream_t st);
 int sgns_blocks_per_cu(int K, int nv);
 hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
                                int64_t ld, int nvec, hipStream_t st);
