@@ -20,7 +20,8 @@ K_COMPILED = (1, 2, 3, 5, 10, 15, 20)  # == G2V_FOR_EACH_K in g2v_internal.h
 UNITS = ([("g2v_sgns_atomic.hip", [f"-DG2V_K={k}"], f"g2v_sgns_atomic_k{k}.o") for k in K_COMPILED]
          + [("g2v_sgns.hip", [f"-DG2V_K={k}"], f"g2v_sgns_k{k}.o") for k in K_COMPILED]
          + [(s, [], os.path.splitext(s)[0] + ".o")
-            for s in ("g2v_kernels.hip", "g2v_api.hip", "g2v_host.cpp", "g2v_ingest.cpp")])
+            for s in ("g2v_kernels.hip", "g2v_api.hip", "g2v_coexpr.hip", "g2v_host.cpp",
+                      "g2v_ingest.cpp")])
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(CSRC, "g2v_device.h"),
            os.path.join(ROOT, "include", "g2v.h")]

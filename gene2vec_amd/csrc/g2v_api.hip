@@ -85,6 +85,11 @@ int dev_reserve(hipStream_t st, T** p, int64_t* cap, int64_t need) {
 
 }  // namespace
 
+int g2v::set_error(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
 struct g2v_ctx {
   int device = 0;
   int32_t V = 0, D = 0, K = 0, window = 1;

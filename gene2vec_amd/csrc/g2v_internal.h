@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace g2v {
 
 // gensim 3.4.0 constants ([ext] word2vec_inner.pyx, base_any2vec.py)
@@ -111,6 +113,9 @@ hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
                         double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
                         hipStream_t st);
+
+// record an error for g2v_last_error() (g2v_api.hip); returns code
+int set_error(int code, const std::string& msg);
 
 // host side: LCG jump tables (g2v_host.cpp)
 void lcg_jump_tables(uint64_t* a_lo, uint64_t* c_lo, uint64_t* a_hi, uint64_t* c_hi);

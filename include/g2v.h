@@ -182,6 +182,18 @@ int g2v_sync(g2v_ctx *ctx);
 /* Accumulated since the previous call (synchronises, then resets). */
 int g2v_read_stats(g2v_ctx *ctx, g2v_stats *out);
 
+/* ---- producer side: co-expression pairs -------------------------------------- */
+/* Replaces the per-study coexpr() of src/generate_gene_pairs.py:45-65:
+ * corr = data.corr().abs(); (corr > threshold).values.nonzero(); row != col.
+ * x: host [n_samples][n_genes] fp64 row-major (DataFrame.values; no NaN).
+ * Writes the (row, col) gene-index pairs, both orders, no diagonal, in
+ * nonzero() order (row-major) to pairs[n][2] when pairs != NULL and cap >= n;
+ * *n_pairs always receives n (G2V_ERANGE when cap < n).  Columns with zero
+ * variance never pair (pandas: NaN).  Standalone (own device buffers),
+ * synchronises. */
+int g2v_coexpr_pairs(int device, const double *x, int64_t n_samples, int64_t n_genes,
+                     double threshold, int32_t *pairs, int64_t cap, int64_t *n_pairs);
+
 /* ---- consumer side ----------------------------------------------------------------- */
 /* gensim wv.similarity for n index pairs (src/evaluation_target_function.py:38,49):
  * out[i] = dot(unitvec(v[a[i]]), unitvec(v[b[i]])), unitvec = v * (1/||v||) in

@@ -13,6 +13,10 @@ Contents
 ``sgns_oracle.c``   The same semantics in C (sequential "workers=1" order and a
                     Hogwild OpenMP variant used as the CPU baseline).
 ``Makefile``        Builds ``oracle/build/liboracle.so`` from ``sgns_oracle.c``.
+``target_oracle.py`` ``src/evaluation_target_function.py`` restated (numpy).
+``coexpr_oracle.py`` ``src/generate_gene_pairs.py:45-65`` (coexpr) through
+                    pandas' own ``DataFrame.corr`` -- the reference's library,
+                    importable here, so this path's parity IS pinned.
 
 Parity status: **parity unpinned.**  The algorithm lives in gensim 3.4.0
 (``gensim/models/word2vec_inner.pyx``, ``word2vec.py``, ``base_any2vec.py``),

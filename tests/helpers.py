@@ -39,3 +39,55 @@ def vocab_from_ids(pairs_flat, V):
     remap = np.full(V, -1, dtype=np.int32)
     remap[order] = np.arange(len(order), dtype=np.int32)
     return order, remap, counts[order].astype(np.int64)
+
+
+def planted_expression(n_samples, n_genes, n_groups=4, noise=0.15, seed=0, zeros=0.0):
+    """[samples][genes] positive expression with planted co-expressed groups:
+    gene g follows latent factor g % n_groups with loading and noise; a
+    fraction `zeros` of entries set to 0 (TPM dropouts)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    f = rng.normal(size=(n_samples, n_groups))
+    load = rng.uniform(0.5, 2.0, size=n_genes) * rng.choice([-1.0, 1.0], size=n_genes)
+    x = f[:, np.arange(n_genes) % n_groups] * load + noise * rng.normal(size=(n_samples, n_genes))
+    x = np.exp(x)
+    if zeros:
+        x[rng.random(x.shape) < zeros] = 0.0
+    return x
+
+
+def make_query(root, seed=0, studies=(("SRP1", 24), ("SRP2", 30), ("SRP3", 5)), n_genes=150):
+    """Synthetic processed query in the layout src/generate_gene_pairs.py:143-155
+    reads: data/SRARunTable.csv, data/gene_counts_TPM.csv, data/gene_counts.csv.
+    Gene ids 'ENSG<k>|NAME<k>' with some unnamed, some duplicated names and
+    some low-count genes."""
+    import os
+
+    import pandas as pd
+
+    rng = np.random.Generator(np.random.PCG64(seed + 1000))
+    runs, study_of = [], []
+    for s, n in studies:
+        for i in range(n):
+            runs.append(f"{s}_R{i:03d}")
+            study_of.append(s)
+    x = planted_expression(len(runs), n_genes, seed=seed, zeros=0.05)
+    ens = [f"ENSG{k:05d}" for k in range(n_genes)]
+    ids = []
+    for k, e in enumerate(ens):
+        if k % 17 == 3:
+            ids.append(e)                       # no name -> dropped by name mode
+        elif k % 23 == 5:
+            ids.append(f"{e}|DUP{k % 2}")        # duplicated names -> dropped
+        else:
+            ids.append(f"{e}|G{k}")
+    counts = rng.integers(0, 40, size=(n_genes, len(runs)))
+    counts[::11] = 0                             # low-expression genes
+    os.makedirs(os.path.join(root, "data"), exist_ok=True)
+    pd.DataFrame({"SRA Study": study_of}, index=pd.Index(runs, name="Run")).to_csv(
+        os.path.join(root, "data/SRARunTable.csv"))
+    pd.DataFrame(x, index=pd.Index(runs, name="Run"), columns=ens).to_csv(
+        os.path.join(root, "data/gene_counts_TPM.csv"))
+    gc = pd.DataFrame(counts, columns=runs)
+    gc.insert(0, "gene_id", ids)
+    gc.to_csv(os.path.join(root, "data/gene_counts.csv"), index=False)
+    return root
