@@ -35,6 +35,7 @@ if ROOT not in sys.path:
 import numpy as np  # noqa: E402
 
 METRIC = "gene pairs/sec (SGNS dim200 neg5) at 1/2/4/8 MI355X + achieved GB/s"
+# BASELINE.json configs[3] (C4): python bench.py --vocab 60000 --dim 512 --negative 15
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
@@ -233,6 +234,7 @@ def main():
                "sample": f"first {ns} pairs of the same corpus, 1 epoch, C oracle "
                          f"(oracle/sgns_oracle.c) Hogwild OpenMP, {dt:.2f} s"}
 
+    cfg_name = {(24447, 200, 5): "C2", (60000, 512, 15): "C4"}.get((V0, D, K), "custom")
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "pairs/s", "n_gpus": world,
@@ -240,10 +242,11 @@ def main():
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {
-                "workload": ("C2: synthetic Zipf(1.0) gene pairs, V=24447, 100M pairs, dim 200, "
-                             "neg 5, window 1, sample 1e-3, 1 epoch per step") if world == 1 else
-                            (f"C3: synthetic Zipf gene pairs, V=24447, {n_pairs} pairs per GPU x "
-                             f"{world}, dim 200, neg 5, RCCL row-wise replica merge ({a.merge}) "
+                "workload": (f"{cfg_name}: synthetic Zipf({a.zipf:g}) gene pairs, V={V0}, "
+                             f"{n_pairs} pairs, dim {D}, neg {K}, window 1, sample {a.sample:g}, "
+                             "1 epoch per step") if world == 1 else
+                            (f"C3: synthetic Zipf gene pairs, V={V0}, {n_pairs} pairs per GPU x "
+                             f"{world}, dim {D}, neg {K}, RCCL row-wise replica merge ({a.merge}) "
                              f"every {avg_every} jobs"),
                 "vocab": V, "pairs_per_gpu": n_pairs, "dim": D, "negative": K,
                 "sample": a.sample, "window": 1,
