@@ -63,7 +63,9 @@ __global__ void k_coexpr_stats(const double* __restrict__ x, int64_t n, int64_t 
   for (int64_t k = 0; k < n; ++k) z[k * gp + g] = (x[k * G + g] - mean) * inv;
 }
 
-// grid (gp/64, gp/64), 256 threads; z is [npad][gp] (padding rows/cols zero)
+// grid (gp/64, gp/64), 256 threads; z is [npad][gp] (padding rows/cols zero).
+// corr is symmetric: only tiles with bx >= by compute; an off-diagonal tile
+// also writes its transposed bits (row c, column block by)
 __global__ __launch_bounds__(256) void k_coexpr_mask(const double* __restrict__ z, int64_t npad,
                                                      int64_t gp, int64_t G,
                                                      const uint8_t* __restrict__ cst,
@@ -71,10 +73,15 @@ __global__ __launch_bounds__(256) void k_coexpr_mask(const double* __restrict__ 
   __shared__ double sa[kKt][kTile];
   __shared__ double sb[kKt][kTile];
   __shared__ unsigned long long sm[kTile];
+  __shared__ unsigned long long smt[kTile];
+  if (blockIdx.x < blockIdx.y) return;
   const int t = threadIdx.x;
   const int ty = t >> 4, tx = t & 15;
   const int64_t r0 = (int64_t)blockIdx.y * kTile, c0 = (int64_t)blockIdx.x * kTile;
-  if (t < kTile) sm[t] = 0ull;
+  if (t < kTile) {
+    sm[t] = 0ull;
+    smt[t] = 0ull;
+  }
   double acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -105,6 +112,7 @@ __global__ __launch_bounds__(256) void k_coexpr_mask(const double* __restrict__ 
     }
     __syncthreads();
   }
+  unsigned long long colbits[4] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int64_t r = r0 + ty * 4 + i;
@@ -114,11 +122,21 @@ __global__ __launch_bounds__(256) void k_coexpr_mask(const double* __restrict__ 
       const int64_t c = c0 + tx * 4 + j;
       const bool on = r < G && c < G && r != c && !cst[r] && !cst[c] && fabs(acc[i][j]) > thr;
       bits |= (unsigned long long)on << (tx * 4 + j);
+      colbits[j] |= (unsigned long long)on << (ty * 4 + i);
     }
     if (bits) atomicOr(&sm[ty * 4 + i], bits);
   }
+  const bool offdiag = blockIdx.x != blockIdx.y;
+  if (offdiag) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (colbits[j]) atomicOr(&smt[tx * 4 + j], colbits[j]);
+  }
   __syncthreads();
-  if (t < kTile) mask[(r0 + t) * (gp / kTile) + blockIdx.x] = sm[t];
+  if (t < kTile) {
+    mask[(r0 + t) * (gp / kTile) + blockIdx.x] = sm[t];
+    if (offdiag) mask[(c0 + t) * (gp / kTile) + blockIdx.y] = smt[t];
+  }
 }
 
 __global__ void k_coexpr_count(const uint64_t* __restrict__ mask, int64_t gp,
