@@ -34,6 +34,8 @@ OPT_STRIPE_ROWS = 7
 OPT_STRIPE_COPIES = 8
 BATCH_WORDS = 10000
 MAX_DIM = 512
+TXT_MATRIX = 0
+TXT_W2V = 1
 SUPPORTED_NEGATIVE = (1, 2, 3, 5, 10, 15, 20)
 
 
@@ -85,6 +87,9 @@ SIGNATURES = {
     "g2v_read_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "g2v_cosine_pairs": (C.c_int, [C.c_int, _vp, _i64, _i32, _vp, _vp, _i64, _vp]),
     "g2v_seeded_vectors": (C.c_int, [_vp, _i64, _i32, _vp]),
+    "g2v_format_rows": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _i32, _vp, _i64,
+                                  C.POINTER(_i64)]),
+    "g2v_format_f32": (C.c_int, [_vp, _i64, _vp, _i64, C.POINTER(_i64)]),
     "g2v_coexpr_pairs": (C.c_int, [C.c_int, _vp, _i64, _i64, _f64, _vp, _i64, C.POINTER(_i64)]),
     "g2v_count_ids": (C.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "g2v_corpus_read": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.POINTER(_vp)]),

@@ -21,7 +21,7 @@ UNITS = ([("g2v_sgns_atomic.hip", [f"-DG2V_K={k}"], f"g2v_sgns_atomic_k{k}.o") f
          + [("g2v_sgns.hip", [f"-DG2V_K={k}"], f"g2v_sgns_k{k}.o") for k in K_COMPILED]
          + [(s, [], os.path.splitext(s)[0] + ".o")
             for s in ("g2v_kernels.hip", "g2v_api.hip", "g2v_coexpr.hip", "g2v_host.cpp",
-                      "g2v_ingest.cpp")])
+                      "g2v_ingest.cpp", "g2v_export.cpp")])
 SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(CSRC, "g2v_device.h"),
            os.path.join(ROOT, "include", "g2v.h")]

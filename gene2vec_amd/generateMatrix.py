@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import numpy as np
 
+from . import textio
 from .word2vec import KeyedVectors
 
 
@@ -24,8 +25,8 @@ def load_embeddings(file_name):
 def outputTxt(embeddings_file):
     wv, vocabulary = load_embeddings(embeddings_file)
     matrix_txt_file = embeddings_file + ".txt"
-    rows = wv.astype(np.float32).astype(str)  # == str(np.float32(v)) element-wise
-    with open(matrix_txt_file, "w") as out:
-        for word, vals in zip(vocabulary, rows):
-            out.write(str(word) + "\t" + "".join(v + " " for v in vals) + "\n")
+    # str(np.float32(v)) per value, formatted natively (gene2vec_amd.textio)
+    text = textio.format_rows(wv.astype(np.float32), None, vocabulary, textio.TXT_MATRIX)
+    with open(matrix_txt_file, "wb") as out:
+        out.write(text)
     return matrix_txt_file

@@ -165,9 +165,10 @@ class KeyedVectors:
                     row = self.vectors[voc.index].astype("<f4")
                     f.write(word.encode("utf-8") + b" " + row.tobytes())
             else:
-                rows = self.vectors[[voc.index for _, voc in order]].astype(REAL).astype(str)
-                for (word, _), vals in zip(order, rows):
-                    f.write((word + " " + " ".join(vals) + "\n").encode("utf-8"))
+                from . import textio
+                f.write(textio.format_rows(self.vectors.astype(REAL, copy=False),
+                                           [voc.index for _, voc in order],
+                                           [word for word, _ in order], textio.TXT_W2V))
 
     @classmethod
     def load_word2vec_format(cls, fname, binary=False, encoding="utf8",

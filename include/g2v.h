@@ -182,6 +182,24 @@ int g2v_sync(g2v_ctx *ctx);
 /* Accumulated since the previous call (synchronises, then resets). */
 int g2v_read_stats(g2v_ctx *ctx, g2v_stats *out);
 
+/* ---- text exporters ------------------------------------------------------------- */
+/* Row text of the two exporters, every float32 printed as numpy's
+ * str(np.float32(v)) (shortest round-trip digits; positional for
+ * 1e-4 <= |v| < 1e16 and 0, else scientific with a >= 2-digit exponent):
+ *   G2V_TXT_MATRIX  src/generateMatrix.py:18-24: word '\t' (str(v) ' ')*D '\n'
+ *   G2V_TXT_W2V     [ext] save_word2vec_format(binary=False) rows:
+ *                   word ' ' str(v) joined by ' ' '\n'
+ * Line k prints vectors[rows[k]] (rows NULL = k) with ld floats per row and
+ * the word words[word_off[k] .. word_off[k+1]).  out NULL: *written gets the
+ * byte count only; otherwise G2V_ERANGE when cap is too small.  Host only. */
+#define G2V_TXT_MATRIX 0
+#define G2V_TXT_W2V 1
+int g2v_format_rows(const float *vectors, int64_t ld, int32_t D, const int64_t *rows,
+                    int64_t n_rows, const char *words, const int64_t *word_off, int32_t style,
+                    char *out, int64_t cap, int64_t *written);
+/* x[i] as str(np.float32(x[i])), one per line (test hook for the formatter). */
+int g2v_format_f32(const float *x, int64_t n, char *out, int64_t cap, int64_t *written);
+
 /* ---- producer side: co-expression pairs -------------------------------------- */
 /* Replaces the per-study coexpr() of src/generate_gene_pairs.py:45-65:
  * corr = data.corr().abs(); (corr > threshold).values.nonzero(); row != col.

@@ -126,3 +126,42 @@ def test_cli_ingest(tmp_path):
     pairs = read_gene_pairs(str(d), "txt", random.Random(0))
     assert sorted(map(tuple, pairs)) == sorted(
         [("G1", "G2"), ("Gé", "G3"), (), ("G1", "G3"), ("G4", "G5")])
+
+
+def _py_txt(words, rows):
+    # src/generateMatrix.py:18-24 in pure Python
+    return "".join(str(w) + "\t" + "".join(str(v) + " " for v in r) + "\n"
+                   for w, r in zip(words, rows)).encode("utf-8")
+
+
+def _py_w2v(words, rows):
+    # [ext] save_word2vec_format(binary=False) row text
+    return "".join(w + " " + " ".join(str(v) for v in r) + "\n"
+                   for w, r in zip(words, rows)).encode("utf-8")
+
+
+def test_native_row_formatter_matches_python_exporters():
+    from gene2vec_amd import textio
+    rng = np.random.default_rng(3)
+    v = (rng.standard_normal((300, 37)) * rng.choice([1e-6, 0.3, 1e5], size=(300, 1)))
+    v = v.astype(np.float32)
+    v[0, :6] = [0.0, -0.0, np.inf, -np.inf, np.nan, 1e-4]
+    words = [f"G{i}" for i in range(299)] + ["Gé"]
+    order = rng.permutation(300)
+    assert textio.format_rows(v, None, words, textio.TXT_MATRIX) == _py_txt(words, v)
+    assert textio.format_rows(v, order, [words[i] for i in order], textio.TXT_W2V) == \
+        _py_w2v([words[i] for i in order], v[order])
+    assert textio.format_rows(v[:0], None, [], textio.TXT_W2V) == b""
+
+
+def test_float32_formatter_on_random_bit_patterns():
+    import ctypes as C
+
+    from gene2vec_amd import _native as N
+    bits = np.random.default_rng(5).integers(0, 2 ** 32, 300_000, dtype=np.uint64)
+    x = bits.astype(np.uint32).view(np.float32)
+    buf = np.empty(len(x) * 24, np.uint8)
+    w = C.c_int64()
+    N.check(N.lib().g2v_format_f32(N.ptr(x), len(x), N.ptr(buf), len(buf), C.byref(w)))
+    got = bytes(buf[:w.value]).decode().split("\n")[:-1]
+    assert got == x.astype(str).tolist()
