@@ -240,15 +240,49 @@ int g2v_csr_permute(const int32_t* tok, const int64_t* off, int64_t n_sent, cons
   if (n_sent < 0 || (n_sent > 0 && (!tok || !off || !perm || !out_tok || !out_off)))
     return G2V_EINVAL;
   out_off[0] = 0;
-  for (int64_t i = 0; i < n_sent; ++i) {
-    const int64_t p = perm[i];
-    if (p < 0 || p >= n_sent) return G2V_EINVAL;
-    out_off[i + 1] = out_off[i] + (off[p + 1] - off[p]);
-  }
-  for (int64_t i = 0; i < n_sent; ++i) {
-    const int64_t p = perm[i];
-    memcpy(out_tok + out_off[i], tok + off[p], sizeof(int32_t) * (off[p + 1] - off[p]));
-  }
+  // lengths (parallel) -> offsets (block-parallel scan) -> gather (parallel)
+  const int nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, n_sent >> 16));
+  std::atomic<bool> bad{false};
+  std::vector<int64_t> part((size_t)nt + 1, 0);
+  auto run = [&](auto&& fn) {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
+    fn(0);
+    for (auto& x : th) x.join();
+  };
+  run([&](int t) {
+    const int64_t a = n_sent * t / nt, b = n_sent * (t + 1) / nt;
+    int64_t sum = 0;
+    for (int64_t i = a; i < b; ++i) {
+      const int64_t p = perm[i];
+      if (p < 0 || p >= n_sent) {
+        bad = true;
+        return;
+      }
+      sum += off[p + 1] - off[p];
+      out_off[i + 1] = sum;
+    }
+    part[(size_t)t + 1] = sum;
+  });
+  if (bad) return G2V_EINVAL;
+  for (int t = 0; t < nt; ++t) part[(size_t)t + 1] += part[(size_t)t];
+  run([&](int t) {
+    const int64_t a = n_sent * t / nt, b = n_sent * (t + 1) / nt;
+    const int64_t base = part[(size_t)t];
+    for (int64_t i = a; i < b; ++i) {
+      out_off[i + 1] += base;
+      const int64_t p = perm[i];
+      const int64_t len = off[p + 1] - off[p];
+      const int32_t* src = tok + off[p];
+      int32_t* dst = out_tok + (out_off[i + 1] - len);
+      if (len == 2) {
+        dst[0] = src[0];
+        dst[1] = src[1];
+      } else {
+        memcpy(dst, src, sizeof(int32_t) * len);
+      }
+    }
+  });
   return G2V_OK;
 }
 
@@ -295,13 +329,27 @@ struct PyMT {
 };
 }  // namespace
 
+int g2v_py_shuffle_range(uint32_t* state624, uint32_t* pos, int64_t* x, int64_t n) {
+  if (n > 0 && !x) return G2V_EINVAL;
+  for (int64_t i = 0; i < n; ++i) x[i] = i;
+  return g2v_py_shuffle(state624, pos, x, n);
+}
+
 int g2v_py_shuffle(uint32_t* state624, uint32_t* pos, int64_t* x, int64_t n) {
   if (!state624 || !pos || (n > 0 && !x)) return G2V_EINVAL;
   if (n > ((int64_t)1 << 32)) return G2V_ERANGE;
   PyMT r{state624, pos};
-  for (int64_t i = n - 1; i >= 1; --i) {
-    const int64_t j = (int64_t)r.randbelow((uint64_t)(i + 1));
-    std::swap(x[i], x[j]);
+  // same swaps in the same order; the j of a block are drawn first so the
+  // random x[j] lines can be prefetched ahead of their swap
+  constexpr int kB = 4096, kAhead = 24;
+  std::vector<int64_t> js(kB);
+  for (int64_t hi = n - 1; hi >= 1; hi -= kB) {
+    const int64_t cnt = std::min<int64_t>(kB, hi);
+    for (int64_t k = 0; k < cnt; ++k) js[(size_t)k] = (int64_t)r.randbelow((uint64_t)(hi - k + 1));
+    for (int64_t k = 0; k < cnt; ++k) {
+      if (k + kAhead < cnt) __builtin_prefetch(x + js[(size_t)(k + kAhead)], 1);
+      std::swap(x[hi - k], x[js[(size_t)k]]);
+    }
   }
   return G2V_OK;
 }

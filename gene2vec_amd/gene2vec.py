@@ -107,8 +107,10 @@ def main(argv=None):
         n_pairs = len(gene_pairs)
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
+    perm_buf = None
     if corpus is not None:
-        corpus = corpus.permuted(ingest.py_shuffle_perm(corpus.n_sent, rng))
+        perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng)
+        corpus.permute_(perm_buf)
     else:
         rng.shuffle(gene_pairs)
     print(datetime.datetime.now())
@@ -139,7 +141,8 @@ def main(argv=None):
             print(datetime.datetime.now())
             print("shuffle start " + str(n_pairs))
             if corpus is not None:
-                corpus = corpus.permuted(ingest.py_shuffle_perm(corpus.n_sent, rng))
+                perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng, out=perm_buf)
+                corpus.permute_(perm_buf)
             else:
                 rng.shuffle(gene_pairs)
             print(datetime.datetime.now())

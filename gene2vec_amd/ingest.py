@@ -45,6 +45,22 @@ class Corpus:
                                         N.ptr(perm), N.ptr(tok), N.ptr(off)))
         return Corpus(tok, off, self.words, self.counts)
 
+    def permute_(self, perm):
+        """In-place form of ``permuted`` for the per-iteration reshuffle of
+        src/gene2vec.py:80: the sentences are gathered into a spare pair of
+        buffers kept from the previous call (no fresh 2 x 160 MB allocation
+        and page faults per iteration at 20 M pairs), then the buffers swap."""
+        perm = np.ascontiguousarray(perm, dtype=np.int64)
+        spare = getattr(self, "_spare", None)
+        if spare is None or spare[0].shape != self.tokens.shape:
+            spare = (np.empty_like(self.tokens), np.empty_like(self.sent_off))
+        tok, off = spare
+        N.check(N.lib().g2v_csr_permute(N.ptr(self.tokens), N.ptr(self.sent_off), self.n_sent,
+                                        N.ptr(perm), N.ptr(tok), N.ptr(off)))
+        self._spare = (self.tokens, self.sent_off)
+        self.tokens, self.sent_off = tok, off
+        return self
+
     def vocab_raw_counts(self):
         """{word: count} in first-occurrence order of the CURRENT sentence order
         (what gensim's scan_vocab builds), plus ids remapped to that order."""
@@ -80,13 +96,16 @@ def read_corpus(paths, threads=None):
     return Corpus(tok, off, words, counts)
 
 
-def py_shuffle_perm(n, rng: random.Random):
+def py_shuffle_perm(n, rng: random.Random, out=None):
     """permutation p with shuffled[i] = original[p[i]], consuming rng exactly
-    as rng.shuffle(list_of_length_n) does."""
+    as rng.shuffle(list_of_length_n) does (``out``: int64[n] buffer to reuse)."""
     version, internal, gauss = rng.getstate()
     state = np.array(internal[:624], dtype=np.uint32)
     pos = np.array([internal[624]], dtype=np.uint32)
-    perm = np.arange(n, dtype=np.int64)
-    N.check(N.lib().g2v_py_shuffle(N.ptr(state), N.ptr(pos), N.ptr(perm), n))
+    if out is None or out.shape != (n,) or out.dtype != np.int64:
+        perm = np.empty(n, dtype=np.int64)
+    else:
+        perm = out
+    N.check(N.lib().g2v_py_shuffle_range(N.ptr(state), N.ptr(pos), N.ptr(perm), n))
     rng.setstate((version, tuple(int(x) for x in state) + (int(pos[0]),), gauss))
     return perm

@@ -248,6 +248,8 @@ int g2v_csr_permute(const int32_t *tok, const int64_t *off, int64_t n_sent, cons
 /* CPython random.Random.shuffle(x) bit for bit; state624/pos = getstate()[1][:625],
  * updated in place (setstate afterwards keeps Python's generator in step). */
 int g2v_py_shuffle(uint32_t *state624, uint32_t *pos, int64_t *x, int64_t n);
+/* x = range(n), then g2v_py_shuffle (the permutation gene2vec.py:52,80 applies). */
+int g2v_py_shuffle_range(uint32_t *state624, uint32_t *pos, int64_t *x, int64_t n);
 
 #ifdef __cplusplus
 }
