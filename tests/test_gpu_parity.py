@@ -382,3 +382,46 @@ def test_striping_keeps_values_exact():
     for g0, g1 in outs:
         _close(g0, a0)
         _close(g1, a1)
+
+
+def test_sampler_at_c2_full_size_bit_exact():
+    """BASELINE C2 at full size (V=24447, 100 M pairs, the bench corpus):
+    effective words and directed examples of one production train() equal the
+    C oracle's count, and the sampled records (downsampling + LCG jump-ahead +
+    bisected negatives) of job windows at the start, middle and end of the
+    corpus equal the oracle's bit for bit."""
+    from gene2vec_amd import synthetic as S
+    n, V0 = 100_000_000, 24447
+    pairs = S.zipf_gene_pairs(n, V0, 1.0, seed=20250114)
+    flat = pairs.reshape(-1)
+    del pairs
+    counts, first = E.count_ids(flat, V0)
+    order, remap = S.vocab_order(counts, first)
+    tok = remap[flat]
+    del flat
+    vc = counts[order].astype(np.int64)
+    V = len(order)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    sd = E.job_seeds(np.random.RandomState(1), len(js) - 1)
+    eng = E.SGNSEngine(V, 200, 5)
+    eng.set_vocab(vc, 1e-3)
+    eng.set_corpus(tok, sent_len=2)
+    rng = np.random.Generator(np.random.PCG64(5))
+    eng.set_weights(((rng.random((V, 200)) - 0.5) / 200).astype(np.float32),
+                    np.zeros((V, 200), np.float32))
+    eng.train(js, E.job_alphas(js, n), sd, N.MODE_HOGWILD)
+    st = eng.read_stats()
+    off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
+    si, cum = CO.sample_int(vc, 1e-3), CO.make_cum_table(vc)
+    assert st["raw_words"] == 2 * n and st["jobs"] == len(js) - 1
+    assert st["examples"] == CO.count_records(tok, off, js, sd, si, True, cum, 5)
+    nj = len(js) - 1
+    for j0 in (0, nj // 2, nj - 3):
+        w = js[j0:j0 + 4] - js[j0]
+        s0, s1 = js[j0], js[j0 + 3]
+        sub_tok = tok[2 * s0:2 * s1]
+        ref = CO.sample_records(sub_tok, off[:s1 - s0 + 1], w, sd[j0:j0 + 3], si, True, cum, 5)
+        got = eng.debug_sample(js[j0:j0 + 4], sd[j0:j0 + 3])
+        assert np.array_equal(got, ref), j0
+    g0, g1 = eng.get_weights()
+    assert np.isfinite(g0).all() and np.isfinite(g1).all() and np.abs(g1).max() > 0
