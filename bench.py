@@ -58,6 +58,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-eval", action="store_true")
+    p.add_argument("--no-gather-roof", action="store_true",
+                   help="skip the (untimed) write-free gather-roof measurement")
     p.add_argument("--dist", action="store_true",
                    help="init torch.distributed (RCCL) and average replicas even at N=1")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
@@ -195,6 +197,24 @@ def main():
                                     "of added bytes chip-wide)",
                 "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
                 "atomic_frac": round(atomic_gbps / 1300.0, 4)}
+
+    # ---- measured gather roof: the same kernel on the same index
+    # stream with its table writes compiled out (G2V_OPT_DEBUG_WRITE=2) and a
+    # full-occupancy grid, untimed by the contract, tables left unchanged ----------
+    if rank == 0 and K == 5 and D <= 256 and not a.no_gather_roof:
+        gj = min(n_jobs, 2048)
+        eng.set_option(N.OPT_DEBUG_WRITE, 2)
+        eng.set_option(N.OPT_GRID, 2048)
+        eng.train(js[:gj + 1], alphas[:gj], step_seeds[0][:gj], N.MODE_HOGWILD, timing=True)
+        gs = eng.read_stats()
+        eng.set_option(N.OPT_DEBUG_WRITE, 0)
+        eng.set_option(N.OPT_GRID, a.grid)
+        read_bytes = (K + 2) * D * 4
+        gather_gbps = read_bytes * gs["examples"] / (gs["sgns_kernel_ms"] / 1e3) / 1e9
+        ours = read_bytes * st["examples"] / (st["sgns_kernel_ms"] / 1e3) / 1e9
+        roofline.update({"gather_roof_GBps": round(gather_gbps, 1),
+                         "gather_achieved_GBps": round(ours, 1),
+                         "gather_frac": round(ours / gather_gbps, 4)})
 
     # ---- quality sanity check: SGNS objective on held-in pairs ------------------------------
     quality = None
