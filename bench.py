@@ -54,6 +54,8 @@ def parse():
     p.add_argument("--merge", choices=("touch", "mean"), default="touch",
                    help="replica merge rule (gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
+    p.add_argument("--seg-jobs", type=int, default=0,
+                   help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -109,6 +111,8 @@ def main():
     eng = E.SGNSEngine(V, D, K, device=local)
     if a.grid:
         eng.set_option(N.OPT_GRID, a.grid)
+    if a.seg_jobs:
+        eng.set_option(N.OPT_SEG_JOBS, a.seg_jobs)
     # a dedicated (non-default) stream: g2v kernels, RCCL all-reduces and the
     # timing events are all ordered on it
     stream = torch.cuda.Stream(dev)
