@@ -200,6 +200,10 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
   const int nv = nvec <= 64 ? 1 : 2;
   REQUIRE(sgns_supported(negative, nv), G2V_EINVAL,
           "negative=%d not compiled (supported: 1,2,3,5,10,15,20)", negative);
+  // the update kernels address a table through one buffer resource (32-bit offsets)
+  REQUIRE((int64_t)vocab_size * ((vector_size + 31) / 32 * 32) * 4 < ((int64_t)1 << 31),
+          G2V_EINVAL, "vocab_size=%d x vector_size=%d exceeds the 2 GiB per-table limit",
+          vocab_size, vector_size);
   int ndev = 0;
   HIPCHK(hipGetDeviceCount(&ndev));
   REQUIRE(device >= 0 && device < ndev, G2V_EINVAL, "device %d out of range (%d devices)", device,
