@@ -123,10 +123,11 @@ def main():
     names = S.gene_names(V0)
     seeds = np.array([zlib.crc32((names[i] + "1").encode()) for i in order], np.uint32)
     syn0_h = E.seeded_vectors(seeds, D)  # [ext] seeded_vector, deterministic hash
-    syn0 = torch.zeros((V, ld), dtype=torch.float32, device=dev)
-    syn1 = torch.zeros((V, ld), dtype=torch.float32, device=dev)
+    # both tables in one buffer: a replica merge is one collective per quantity
+    tables = torch.zeros((2, V, ld), dtype=torch.float32, device=dev)
+    syn0, syn1 = tables[0], tables[1]
     syn0[:, :D] = torch.from_numpy(syn0_h).to(dev)
-    eng.bind_tables(syn0.data_ptr(), syn1.data_ptr(), ld, keepalive=(syn0, syn1))
+    eng.bind_tables(syn0.data_ptr(), syn1.data_ptr(), ld, keepalive=(tables,))
     eng.set_vocab(vcounts, a.sample)
     tok_d = torch.from_numpy(tok).to(dev)
     eng.set_corpus_device(tok_d.data_ptr(), tok_d.numel(), sent_len=2, keepalive=tok_d)
@@ -136,7 +137,7 @@ def main():
     rs = np.random.RandomState(Dd.rank_seed(1, rank))  # gensim model.random(seed=1) per rank
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
-    trainer = Dd.ReplicaTrainer(eng, (syn0, syn1), avg_every, N.MODE_HOGWILD, merge=a.merge)
+    trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=a.merge)
     torch.cuda.synchronize(dev)
 
     def step(i, timing):

@@ -85,16 +85,19 @@ def touch_merge_(tensors, olds, beta=1.0, group=None):
     import torch.distributed as dist
     single = not dist.is_initialized() or dist.get_world_size(group) == 1
     for t, old in zip(tensors, olds):
+        # rows are the last dimension: a [2][V][ld] buffer holding both tables
+        # merges with one collective per quantity
         d = t - old
-        cnt = (d != 0).any(dim=1).to(t.dtype)
+        cnt = (d != 0).any(dim=-1).to(t.dtype)
         if not single:
             dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
             dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
         k = torch.clamp(cnt, min=1.0)
         if beta != 1.0:
             k = k ** beta
-        t.copy_(old + d / k[:, None])
-        old.copy_(t)
+        d.div_(k.unsqueeze(-1))
+        old.add_(d)
+        t.copy_(old)
 
 
 class ReplicaTrainer:

@@ -68,6 +68,21 @@ def _worker(rank, world, port, q):
         Dd.touch_merge_([t], olds)
         out["touch"] = t.numpy()
         out["touch_old"] = olds[0].numpy()
+        # both tables in one [2][V][ld] buffer (bench.py's layout): same result
+        # as merging each table on its own
+        g = torch.Generator().manual_seed(rank)
+        both = torch.zeros(2, 5, 3)
+        olds2 = [both.clone()]
+        sep = [both[0].clone(), both[1].clone()]
+        sep_old = [x.clone() for x in sep]
+        upd = (torch.rand(2, 5, 3, generator=g) > 0.6).float() * (rank + 1)
+        both += upd
+        sep[0] += upd[0]
+        sep[1] += upd[1]
+        Dd.touch_merge_([both], olds2)
+        Dd.touch_merge_(sep, sep_old)
+        out["fused"] = both.numpy()
+        out["separate"] = np.stack([x.numpy() for x in sep])
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -128,3 +143,9 @@ def test_touch_merge_rowwise(results):
         assert np.allclose(t[2], 2.0)        # only rank 1
         assert np.allclose(t[3], 0.0)        # untouched
         assert np.array_equal(results[r]["touch_old"], t)
+
+
+def test_touch_merge_fused_buffer_equals_per_table(results):
+    for r in (0, 1):
+        assert np.array_equal(results[r]["fused"], results[r]["separate"])
+    assert np.array_equal(results[0]["fused"], results[1]["fused"])
