@@ -80,3 +80,25 @@ def test_cli_end_to_end(tmp_path, mode, ensembl):
     assert GP.main(args) == 0
     with open(os.path.join(GOLDEN, f"coexpr_query_{mode}.txt")) as f:
         assert out.read_text() == f.read()
+
+
+def test_full_size_study_restricted_to_subset_matches_pandas():
+    """20,000 genes x 100 samples (bench size): the GPU pair set restricted to
+    a random 1,200-gene subset equals pandas on that subset (correlations are
+    pairwise, so the subset's pairs are exactly the full run's pairs among it);
+    the full set is symmetric and diagonal-free."""
+    x = np.log2(planted_expression(100, 20000, n_groups=1000, noise=0.4, seed=1))
+    got = GP.coexpr_indices(x, 0.9)
+    assert len(got) > 10000
+    assert not (got[:, 0] == got[:, 1]).any()
+    s = set(map(tuple, got.tolist()))
+    assert all((c, r) in s for r, c in list(s)[:20000])
+    sub = np.sort(np.random.default_rng(2).choice(20000, 1200, replace=False))
+    d = pd.DataFrame(x[:, sub])
+    assert O.near_threshold(d, 0.9, 1e-9) == 0
+    want = O.coexpr_indices(d, 0.9)
+    pos = np.full(20000, -1)
+    pos[sub] = np.arange(len(sub))
+    keep = (pos[got[:, 0]] >= 0) & (pos[got[:, 1]] >= 0)
+    mine = np.stack([pos[got[keep, 0]], pos[got[keep, 1]]], axis=1)
+    np.testing.assert_array_equal(mine, want)
