@@ -268,39 +268,48 @@ extern "C" int g2v_coexpr_pairs(int device, const double* x, int64_t n_samples, 
   const int64_t gp = (G + kTile - 1) / kTile * kTile;
   const int64_t npad = (n + kKt - 1) / kKt * kKt;
   const int64_t words = gp / kTile;
-  DevBuf dx, dz, dc, dm, dn, doff, dp;
+  // one workspace allocation, carved into 256-B aligned pieces
+  auto al = [](int64_t b) { return (b + 255) / 256 * 256; };
+  const int64_t o_x = 0, o_z = o_x + al(8 * n * G), o_m = o_z + al(8 * npad * gp),
+                o_n = o_m + al(8 * gp * words), o_off = o_n + al(8 * gp),
+                o_c = o_off + al(8 * (gp + 1)), ws_bytes = o_c + al(G);
+  DevBuf ws, dp;
   hipStream_t st = nullptr;
   int64_t total = 0;
   CX_CHK(hipSetDevice(device));
   CX_CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  CX_CHK(hipMalloc(&dx.p, sizeof(double) * n * G));
-  CX_CHK(hipMalloc(&dz.p, sizeof(double) * npad * gp));
-  CX_CHK(hipMalloc(&dc.p, (size_t)G));
-  CX_CHK(hipMalloc(&dm.p, sizeof(uint64_t) * gp * words));
-  CX_CHK(hipMalloc(&dn.p, sizeof(int64_t) * gp));
-  CX_CHK(hipMalloc(&doff.p, sizeof(int64_t) * (gp + 1)));
-  CX_CHK(hipMemcpyAsync(dx.p, x, sizeof(double) * n * G, hipMemcpyHostToDevice, st));
-  CX_CHK(hipMemsetAsync(dz.p, 0, sizeof(double) * npad * gp, st));
-  hipLaunchKernelGGL(k_coexpr_stats, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st,
-                     (const double*)dx.p, n, G, gp, (double*)dz.p, (uint8_t*)dc.p);
-  CX_CHK(hipGetLastError());
-  hipLaunchKernelGGL(k_coexpr_mask_mfma, dim3((unsigned)words, (unsigned)words), dim3(256), 0, st,
-                     (const double*)dz.p, npad, gp, G, (const uint8_t*)dc.p, threshold,
-                     (uint64_t*)dm.p);
-  CX_CHK(hipGetLastError());
-  hipLaunchKernelGGL(k_coexpr_count, dim3((unsigned)((gp + 3) / 4)), dim3(256), 0, st,
-                     (const uint64_t*)dm.p, gp, (int64_t*)dn.p);
-  CX_CHK(hipGetLastError());
-  hipLaunchKernelGGL(k_coexpr_scan, dim3(1), dim3(1024), 0, st, (const int64_t*)dn.p, G,
-                     (int64_t*)doff.p);
-  CX_CHK(hipGetLastError());
-  CX_CHK(hipMemcpyAsync(&total, (int64_t*)doff.p + G, sizeof total, hipMemcpyDeviceToHost, st));
-  CX_CHK(hipStreamSynchronize(st));
+  CX_CHK(hipMalloc(&ws.p, (size_t)ws_bytes));
+  {
+    char* base = (char*)ws.p;
+    double* dx = (double*)(base + o_x);
+    double* dz = (double*)(base + o_z);
+    uint64_t* dm = (uint64_t*)(base + o_m);
+    int64_t* dn = (int64_t*)(base + o_n);
+    int64_t* doff = (int64_t*)(base + o_off);
+    uint8_t* dc = (uint8_t*)(base + o_c);
+    CX_CHK(hipMemcpyAsync(dx, x, sizeof(double) * n * G, hipMemcpyHostToDevice, st));
+    CX_CHK(hipMemsetAsync(dz, 0, sizeof(double) * npad * gp, st));
+    hipLaunchKernelGGL(k_coexpr_stats, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st,
+                       (const double*)dx, n, G, gp, dz, dc);
+    CX_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_coexpr_mask_mfma, dim3((unsigned)words, (unsigned)words), dim3(256), 0,
+                       st, (const double*)dz, npad, gp, G, (const uint8_t*)dc, threshold, dm);
+    CX_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_coexpr_count, dim3((unsigned)((gp + 3) / 4)), dim3(256), 0, st,
+                       (const uint64_t*)dm, gp, dn);
+    CX_CHK(hipGetLastError());
+    hipLaunchKernelGGL(k_coexpr_scan, dim3(1), dim3(1024), 0, st, (const int64_t*)dn, G, doff);
+    CX_CHK(hipGetLastError());
+    CX_CHK(hipMemcpyAsync(&total, doff + G, sizeof total, hipMemcpyDeviceToHost, st));
+    CX_CHK(hipStreamSynchronize(st));
+  }
   *n_pairs = total;
   if (pairs && total > 0 && cap >= total) {
     CX_CHK(hipMalloc(&dp.p, sizeof(int32_t) * 2 * total));
+    char* base = (char*)ws.p;
     hipLaunchKernelGGL(k_coexpr_emit, dim3((unsigned)((G + 3) / 4)), dim3(256), 0, st,
-                       (const uint64_t*)dm.p, gp, G, (const int64_t*)doff.p, (int32_t*)dp.p);
+                       (const uint64_t*)(base + o_m), gp, G, (const int64_t*)(base + o_off),
+                       (int32_t*)dp.p);
     CX_CHK(hipGetLastError());
     CX_CHK(hipMemcpyAsync(pairs, dp.p, sizeof(int32_t) * 2 * total, hipMemcpyDeviceToHost, st));
     CX_CHK(hipStreamSynchronize(st));
