@@ -186,8 +186,12 @@ def main():
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
-            if tj.get("vocab") == V0 and tj.get("dim") == D and tj.get("negative") == K:
-                traffic = tj.get("hbm_bytes_per_launch")
+            # per-example PMC bytes of the same workload (vocabulary, shape, downsampling
+            # and skew), scaled to this run's examples per launch
+            if (tj.get("vocab"), tj.get("dim"), tj.get("negative"), tj.get("sample"),
+                    tj.get("zipf")) == (V0, D, K, a.sample, a.zipf):
+                traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
+                                * st["examples"] / launches, 1)
         except Exception:
             traffic = None
     atomic_bytes = (K + 2) * D * 4  # every SGNS update is a memory-side f32 atomic delta

@@ -11,7 +11,7 @@ js = E.plan_jobs(n_sent=NP, sent_len=2); al = E.job_alphas(js, NP)
 rng = np.random.Generator(np.random.PCG64(1)); syn0 = ((rng.random((V, D)) - 0.5) / D).astype(np.float32)
 for spec in sys.argv[1].split(","):
     wr, grid, H, R = (list(map(int, spec.split(":"))) + [8, 8][len(spec.split(":")) - 2:])[:4]
-    eng = E.SGNSEngine(V, D, K); eng.set_vocab(vc, 1e-3); eng.set_corpus(tok, sent_len=2)
+    eng = E.SGNSEngine(V, D, K); eng.set_vocab(vc, float(os.environ.get("SAMPLE", "1e-3"))); eng.set_corpus(tok, sent_len=2)
     eng.set_weights(syn0, np.zeros((V, D), np.float32)); eng.set_option(N.OPT_DEBUG_WRITE, wr); eng.set_option(N.OPT_GRID, grid); eng.set_option(N.OPT_STRIPE_ROWS, H); eng.set_option(N.OPT_STRIPE_COPIES, R)
     rs = np.random.RandomState(1)
     for it in range(2):

@@ -162,9 +162,13 @@ def test_step_sequential_vs_c_oracle(D, K):
     _close(g1, a1, atol=1e-6)
 
 
-def test_step_hogwild_disjoint_equals_sequential():
-    """examples touching disjoint rows: every update order gives the same result"""
-    D, K, B = 200, 5, 64
+@pytest.mark.parametrize("D,K", [(200, 5), (512, 15), (7, 1), (64, 2), (100, 3), (300, 10),
+                                 (256, 20), (508, 5)])
+def test_step_hogwild_disjoint_equals_sequential(D, K):
+    """examples touching disjoint rows: every update order gives the same
+    result -- the production atomic kernel for every compiled negative count,
+    ragged and wide dimensions"""
+    B = 64
     V = B * (K + 2)
     rng = np.random.Generator(np.random.PCG64(3))
     syn0 = ((rng.random((V, D)) - 0.5) / D * 40).astype(np.float32)

@@ -40,6 +40,8 @@ def test_error_path_without_gpu_is_loud():
     assert b"window" in N.lib().g2v_last_error()
     rc = N.lib().g2v_create(0, 10, 8, 4, 1, C.byref(h))  # negative=4 not compiled
     assert rc == N.G2V_EINVAL
+    rc = N.lib().g2v_create(0, 10, 513, 5, 1, C.byref(h))  # wider than one wave's 2 float4s
+    assert rc == N.G2V_EINVAL
     rc = N.lib().g2v_create(0, 3_000_000, 200, 5, 1, C.byref(h))  # > 2 GiB per table
     assert rc == N.G2V_EINVAL and b"2 GiB" in N.lib().g2v_last_error()
 
