@@ -17,73 +17,150 @@
 //  * an empty / whitespace-only line is an empty sentence (kept).
 #include <stdint.h>
 #include <stdio.h>
+#include <fcntl.h>
 #include <string.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
+#include <memory>
 #include <new>
 #include <string>
 #include <string_view>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 #include "g2v.h"
 
 namespace {
 
-inline bool is_sep(unsigned char c) {
-  return c == ' ' || (c >= 0x09 && c <= 0x0d) || (c >= 0x1c && c <= 0x1f) || c == 0xa0;
-}
-inline bool is_undefined_cp1252(unsigned char c) {
-  return c == 0x81 || c == 0x8d || c == 0x8f || c == 0x90 || c == 0x9d;
+// byte classes of the tokenizer: 0 word byte, 1 str.split() separator,
+// 2 line terminator ('\n' / '\r'), 3 byte undefined in windows-1252 (Python's
+// decoder raises UnicodeDecodeError)
+struct ByteClass {
+  uint8_t c[256];
+  constexpr ByteClass() : c() {
+    for (int i = 0; i < 256; ++i) c[i] = 0;
+    c[' '] = 1;
+    for (int i = 0x09; i <= 0x0d; ++i) c[i] = 1;
+    for (int i = 0x1c; i <= 0x1f; ++i) c[i] = 1;
+    c[0xa0] = 1;
+    c['\n'] = 2;
+    c['\r'] = 2;
+    c[0x81] = c[0x8d] = c[0x8f] = c[0x90] = c[0x9d] = 3;
+  }
+};
+constexpr ByteClass kClass{};
+
+inline uint64_t hash_bytes(const unsigned char* p, size_t n) {
+  uint64_t h = 0x9e3779b97f4a7c15ull ^ (uint64_t)n;
+  while (n >= 8) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    h = (h ^ v) * 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 31;
+    p += 8;
+    n -= 8;
+  }
+  uint64_t v = 0;
+  for (size_t i = 0; i < n; ++i) v |= (uint64_t)p[i] << (8 * i);
+  h = (h ^ v) * 0x94d049bb133111ebull;
+  h ^= h >> 29;
+  h *= 0xbf58476d1ce4e5b9ull;
+  return h ^ (h >> 32);
 }
 
-struct Chunk {  // one file (or a line-aligned piece of one)
+struct Chunk {  // a line-aligned piece of one file
   const char* p = nullptr;
   size_t n = 0;
   std::vector<int32_t> tok;              // local ids
   std::vector<int64_t> len;              // sentence lengths
   std::vector<std::string_view> words;   // local id -> bytes (views into the file buffer)
+  std::vector<uint64_t> hash;            // local id -> hash_bytes(word)
   std::vector<int64_t> cnt;              // local counts
   int err = 0;
-  size_t err_at = 0;
+};
+
+// open-addressing word -> id table (linear probing, load <= 1/2).  A slot
+// holds the hash, the length and the first 16 bytes of its word, so a lookup
+// of a gene name (almost always <= 16 bytes) touches one 32-B slot.
+struct WordTable {
+  struct Slot {
+    uint64_t h;
+    int32_t id;  // -1 = empty
+    uint32_t len;
+    char pfx[16];
+  };
+  std::vector<Slot> slot;
+  uint64_t mask = 0;
+  explicit WordTable(size_t cap = 1 << 16) : slot(cap, Slot{0, -1, 0, {}}), mask(cap - 1) {}
+  // id of w, or the slot index (encoded as -1 - slot) where it would go
+  template <class Words>
+  int64_t find(const Words& words, std::string_view w, uint64_t h) const {
+    uint64_t k = h & mask;
+    for (;;) {
+      const Slot& e = slot[k];
+      if (e.id < 0) return -1 - (int64_t)k;
+      if (e.h == h && e.len == w.size() &&
+          (w.size() <= 16 ? memcmp(e.pfx, w.data(), w.size()) == 0 : words[e.id] == w))
+        return e.id;
+      k = (k + 1) & mask;
+    }
+  }
+  // fill the slot find() returned for a new word; grows at load 1/2
+  void insert(int64_t where, std::string_view w, uint64_t h, int32_t id) {
+    Slot& e = slot[(size_t)(-1 - where)];
+    e.h = h;
+    e.id = id;
+    e.len = (uint32_t)w.size();
+    memcpy(e.pfx, w.data(), std::min<size_t>(16, w.size()));
+    if ((size_t)id * 2 + 2 > slot.size()) {
+      std::vector<Slot> s2(slot.size() * 2, Slot{0, -1, 0, {}});
+      const uint64_t m2 = s2.size() - 1;
+      for (const Slot& o : slot) {
+        if (o.id < 0) continue;
+        uint64_t k = o.h & m2;
+        while (s2[k].id >= 0) k = (k + 1) & m2;
+        s2[k] = o;
+      }
+      slot.swap(s2);
+      mask = m2;
+    }
+  }
 };
 
 void tokenize(Chunk& c) {
-  std::unordered_map<std::string_view, int32_t> ids;
-  ids.reserve(1 << 16);
+  WordTable tab;
   const unsigned char* s = (const unsigned char*)c.p;
-  size_t i = 0, n = c.n;
+  const size_t n = c.n;
+  c.tok.reserve(n / 6 + 16);
+  c.len.reserve(n / 12 + 16);
+  size_t i = 0;
   while (i < n) {
     // one line: up to '\n', '\r\n' or '\r'
     int64_t ntok = 0;
-    while (i < n && s[i] != '\n' && s[i] != '\r') {
-      if (is_sep(s[i])) {
-        ++i;
-        continue;
-      }
+    for (;;) {
+      while (i < n && kClass.c[s[i]] == 1) ++i;
+      if (i >= n || kClass.c[s[i]] == 2) break;
       const size_t b = i;
-      while (i < n && s[i] != '\n' && s[i] != '\r' && !is_sep(s[i])) {
-        if (is_undefined_cp1252(s[i]) && !c.err) {
-          c.err = 1;
-          c.err_at = i;
-        }
+      uint8_t cls;
+      while (i < n && ((cls = kClass.c[s[i]]) == 0 || cls == 3)) {
+        c.err |= cls == 3;
         ++i;
       }
-      std::string_view w((const char*)s + b, i - b);
-      auto it = ids.find(w);
-      int32_t id;
-      if (it == ids.end()) {
-        id = (int32_t)c.words.size();
-        ids.emplace(w, id);
+      const std::string_view w((const char*)s + b, i - b);
+      const uint64_t h = hash_bytes(s + b, i - b);
+      int64_t id = tab.find(c.words, w, h);
+      if (id < 0) {
+        tab.insert(id, w, h, (int32_t)c.words.size());
+        id = (int64_t)c.words.size();
         c.words.push_back(w);
+        c.hash.push_back(h);
         c.cnt.push_back(0);
-      } else {
-        id = it->second;
       }
-      c.cnt[id]++;
-      c.tok.push_back(id);
+      c.cnt[(size_t)id]++;
+      c.tok.push_back((int32_t)id);
       ++ntok;
     }
     c.len.push_back(ntok);
@@ -92,6 +169,19 @@ void tokenize(Chunk& c) {
       else ++i;
     }
   }
+}
+
+template <class Fn>
+void parallel_for(size_t n, int threads, Fn&& fn) {
+  const int nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)threads, n));
+  std::atomic_size_t next{0};
+  auto body = [&]() {
+    for (size_t k; (k = next.fetch_add(1)) < n;) fn(k);
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(body);
+  body();
+  for (auto& t : th) t.join();
 }
 
 }  // namespace
@@ -109,32 +199,53 @@ extern "C" {
 int g2v_corpus_read(const char* const* paths, int n_paths, int n_threads, g2v_corpus** out) {
   if (!out || (n_paths > 0 && !paths) || n_paths < 0) return G2V_EINVAL;
   *out = nullptr;
-  g2v_corpus* cp = new (std::nothrow) g2v_corpus();
+  std::unique_ptr<g2v_corpus> cp(new (std::nothrow) g2v_corpus());
   if (!cp) return G2V_ENOMEM;
+  const int threads = n_threads > 0 ? n_threads : 8;
+  // whole files into owned buffers, 64 MiB pieces read in parallel (pread)
+  constexpr size_t kPiece = (size_t)64 << 20;
   cp->files.resize(n_paths);
+  std::vector<int> fds(n_paths, -1);
+  struct Piece {
+    int f;
+    size_t off, n;
+  };
+  std::vector<Piece> pieces;
+  bool bad = false;
   for (int f = 0; f < n_paths; ++f) {
-    FILE* fp = fopen(paths[f], "rb");
-    if (!fp) {
-      delete cp;
-      return G2V_EINVAL;
+    fds[f] = open(paths[f], O_RDONLY);
+    struct stat st;
+    if (fds[f] < 0 || fstat(fds[f], &st) != 0) {
+      bad = true;
+      break;
     }
-    fseek(fp, 0, SEEK_END);
-    const long sz = ftell(fp);
-    fseek(fp, 0, SEEK_SET);
-    cp->files[f].resize(sz > 0 ? (size_t)sz : 0);
-    if (sz > 0 && fread(&cp->files[f][0], 1, (size_t)sz, fp) != (size_t)sz) {
-      fclose(fp);
-      delete cp;
-      return G2V_EINVAL;
-    }
-    fclose(fp);
+    cp->files[f].resize((size_t)st.st_size);
+    for (size_t o = 0; o < (size_t)st.st_size; o += kPiece)
+      pieces.push_back({f, o, std::min(kPiece, (size_t)st.st_size - o)});
   }
-  // line-aligned chunks of ~64 MiB, in file order
+  std::atomic<bool> io_err{false};
+  if (!bad)
+    parallel_for(pieces.size(), threads, [&](size_t k) {
+      const Piece& p = pieces[k];
+      size_t got = 0;
+      while (got < p.n) {
+        const ssize_t r = pread(fds[p.f], &cp->files[p.f][p.off + got], p.n - got,
+                                (off_t)(p.off + got));
+        if (r <= 0) {
+          io_err = true;
+          return;
+        }
+        got += (size_t)r;
+      }
+    });
+  for (int fd : fds)
+    if (fd >= 0) close(fd);
+  if (bad || io_err) return G2V_EINVAL;
+  // line-aligned chunks of ~16 MiB, in file order
   std::vector<Chunk> chunks;
-  const size_t target = (size_t)64 << 20;
+  const size_t target = (size_t)16 << 20;
   for (auto& buf : cp->files) {
     size_t b = 0;
-    if (buf.empty()) continue;
     while (b < buf.size()) {
       size_t e = std::min(buf.size(), b + target);
       while (e < buf.size() && buf[e - 1] != '\n' && buf[e - 1] != '\r') ++e;
@@ -147,57 +258,47 @@ int g2v_corpus_read(const char* const* paths, int n_paths, int n_threads, g2v_co
       b = e;
     }
   }
-  const int nt = std::max(1, std::min<int>(n_threads > 0 ? n_threads : 8, (int)chunks.size()));
-  {
-    std::vector<std::thread> th;
-    std::atomic_size_t next{0};
-    for (int t = 0; t < nt; ++t)
-      th.emplace_back([&]() {
-        for (size_t k; (k = next.fetch_add(1)) < chunks.size();) tokenize(chunks[k]);
-      });
-    for (auto& t : th) t.join();
-  }
+  parallel_for(chunks.size(), threads, [&](size_t k) { tokenize(chunks[k]); });
   for (auto& c : chunks)
-    if (c.err) {
-      delete cp;
-      return G2V_EINVAL;  // UnicodeDecodeError in the reference
-    }
-  // merge in chunk order: global first occurrence = chunk order + local order
-  std::unordered_map<std::string_view, int32_t> gid;
-  size_t ntok = 0, nsent = 0;
-  for (auto& c : chunks) {
-    ntok += c.tok.size();
-    nsent += c.len.size();
-  }
-  cp->tok.resize(ntok);
-  cp->off.resize(nsent + 1);
+    if (c.err) return G2V_EINVAL;  // UnicodeDecodeError in the reference
+  // global ids in first-occurrence order = chunk order, then local order
+  // (sequential over each chunk's vocabulary only); token remap in parallel
+  WordTable gtab(1 << 16);
   std::vector<std::string_view> gwords;
-  size_t tpos = 0, spos = 0;
-  cp->off[0] = 0;
-  for (auto& c : chunks) {
-    std::vector<int32_t> remap(c.words.size());
+  std::vector<std::vector<int32_t>> remap(chunks.size());
+  std::vector<size_t> tbase(chunks.size() + 1, 0), sbase(chunks.size() + 1, 0);
+  for (size_t k = 0; k < chunks.size(); ++k) {
+    Chunk& c = chunks[k];
+    remap[k].resize(c.words.size());
     for (size_t l = 0; l < c.words.size(); ++l) {
-      auto it = gid.find(c.words[l]);
-      if (it == gid.end()) {
-        const int32_t g = (int32_t)gwords.size();
-        gid.emplace(c.words[l], g);
+      int64_t g = gtab.find(gwords, c.words[l], c.hash[l]);
+      if (g < 0) {
+        gtab.insert(g, c.words[l], c.hash[l], (int32_t)gwords.size());
+        g = (int64_t)gwords.size();
         gwords.push_back(c.words[l]);
         cp->counts.push_back(0);
-        remap[l] = g;
-      } else {
-        remap[l] = it->second;
       }
-      cp->counts[remap[l]] += c.cnt[l];
+      remap[k][l] = (int32_t)g;
+      cp->counts[(size_t)g] += c.cnt[l];
     }
-    for (int32_t t : c.tok) cp->tok[tpos++] = remap[t];
-    for (int64_t L : c.len) {
-      cp->off[spos + 1] = cp->off[spos] + L;
-      ++spos;
-    }
+    tbase[k + 1] = tbase[k] + c.tok.size();
+    sbase[k + 1] = sbase[k] + c.len.size();
   }
+  cp->tok.resize(tbase.back());
+  cp->off.resize(sbase.back() + 1);
+  cp->off[0] = 0;
+  parallel_for(chunks.size(), threads, [&](size_t k) {
+    const Chunk& c = chunks[k];
+    const int32_t* rm = remap[k].data();
+    int32_t* dst = cp->tok.data() + tbase[k];
+    for (size_t i = 0; i < c.tok.size(); ++i) dst[i] = rm[c.tok[i]];
+    int64_t o = (int64_t)tbase[k];
+    int64_t* od = cp->off.data() + sbase[k] + 1;
+    for (size_t i = 0; i < c.len.size(); ++i) od[i] = (o += c.len[i]);
+  });
   cp->words.reserve(gwords.size());
   for (auto& w : gwords) cp->words.emplace_back(w);
-  *out = cp;
+  *out = cp.release();
   return G2V_OK;
 }
 

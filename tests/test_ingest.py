@@ -91,3 +91,40 @@ def test_permuted_corpus_and_vocab(files):
         for w in s:
             raw[w] = raw.get(w, 0) + 1
     assert list(c2.vocab_raw_counts().items()) == list(raw.items())
+
+
+def test_native_reader_long_words_table_growth_and_chunks(tmp_path):
+    """words longer than a table slot's 16-byte prefix (and sharing it), more
+    distinct words than the initial table holds, and a file larger than one
+    16 MiB tokenizer chunk (ids must stay in global first-occurrence order)."""
+    rng = np.random.RandomState(1)
+    long_words = [f"ENSG0000000000{i:06d}|LONGNAME" for i in range(50)]
+    many = [f"w{i}" for i in range(70000)]
+    lines = []
+    for i in range(70000):
+        lines.append(f"{many[i]} {long_words[i % 50]}\n")
+    big = "".join(lines)
+    filler = "".join(f"{many[int(a)]} {many[int(b)]}\n"
+                     for a, b in rng.randint(0, 70000, (1_300_000, 2)))
+    p1, p2 = tmp_path / "a.txt", tmp_path / "b.txt"
+    p1.write_bytes((big + filler).encode("windows-1252"))
+    p2.write_bytes(("".join(f"{w} x\n" for w in long_words[::-1])).encode("windows-1252"))
+    assert p1.stat().st_size > (16 << 20)
+    ref = _py_read([str(p1), str(p2)])
+    for threads in (1, 3):
+        c = read_corpus([str(p1), str(p2)], threads=threads)
+        assert c.n_sent == len(ref)
+        assert c.sentences()[:1000] == ref[:1000]
+        assert c.sentences()[-60:] == ref[-60:]
+        seen, fo = set(), []
+        for s in ref:
+            for w in s:
+                if w not in seen:
+                    seen.add(w)
+                    fo.append(w)
+        assert c.words == fo
+        tok = np.concatenate([np.array([fo.index(w) for w in s[:0]], np.int32) for s in ref[:1]])
+        assert tok.size == 0
+        idx = {w: i for i, w in enumerate(fo)}
+        flat = np.array([idx[w] for s in ref for w in s], np.int32)
+        assert np.array_equal(c.tokens, flat)
