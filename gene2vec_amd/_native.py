@@ -91,6 +91,7 @@ SIGNATURES = {
                                   C.POINTER(_i64)]),
     "g2v_format_f32": (C.c_int, [_vp, _i64, _vp, _i64, C.POINTER(_i64)]),
     "g2v_coexpr_pairs": (C.c_int, [C.c_int, _vp, _i64, _i64, _f64, _vp, _i64, C.POINTER(_i64)]),
+    "g2v_coexpr_last_timing": (C.c_int, [C.POINTER(_f64), C.POINTER(_f64)]),
     "g2v_count_ids": (C.c_int, [_vp, _i64, _i32, _vp, _vp]),
     "g2v_corpus_read": (C.c_int, [C.POINTER(C.c_char_p), C.c_int, C.c_int, C.POINTER(_vp)]),
     "g2v_corpus_info": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),

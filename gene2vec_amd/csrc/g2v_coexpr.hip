@@ -78,20 +78,50 @@ __global__ void k_coexpr_stats(const double* __restrict__ x, int64_t n, int64_t 
 // B[k = l>>4][c = l&15]; D reg q: row (l>>4) + 4q, col l&15.
 typedef double d4_t __attribute__((ext_vector_type(4)));
 
+// LDS row pitch in doubles: rows k and k+1 of a stage land 32 banks apart, so
+// the 32 lanes of each half of a ds_read_b64 (16 genes x 2 samples) hit 64
+// distinct banks
+constexpr int kLds = kTile + 16;
+
+// Block b -> upper-triangle tile (ty, tx), tx >= ty, of a words x words tile
+// grid.  Workgroups are dealt to the 8 XCDs round-robin, so block b runs on
+// XCD b % 8; each XCD gets one contiguous run of row-major tiles, and the row
+// panels those tiles share stay in that XCD's L2.  False for padding blocks.
+__device__ inline bool tri_tile(int64_t b, int64_t nblocks, int64_t words, int64_t* ty,
+                                int64_t* tx) {
+  const int64_t T = words * (words + 1) / 2;
+  const int64_t per = nblocks / 8;  // nblocks is a multiple of 8
+  const int64_t l = (b % 8) * per + b / 8;
+  if (l >= T) return false;
+  // row y starts at s(y) = y*words - y*(y-1)/2; invert with sqrt, then fix up
+  const double wd = 2.0 * (double)words + 1.0;
+  int64_t y = (int64_t)((wd - sqrt(wd * wd - 8.0 * (double)l)) * 0.5);
+  if (y < 0) y = 0;
+  if (y >= words) y = words - 1;
+  auto start = [words](int64_t r) { return r * words - r * (r - 1) / 2; };
+  while (y > 0 && start(y) > l) --y;
+  while (y + 1 < words && start(y + 1) <= l) ++y;
+  *ty = y;
+  *tx = y + (l - start(y));
+  return true;
+}
+
 __global__ __launch_bounds__(256) void k_coexpr_mask_mfma(const double* __restrict__ z,
                                                           int64_t npad, int64_t gp, int64_t G,
                                                           const uint8_t* __restrict__ cst,
                                                           double thr,
                                                           uint64_t* __restrict__ mask) {
-  __shared__ double sa[kKt][kTile];
-  __shared__ double sb[kKt][kTile];
+  __shared__ double sa[kKt][kLds];
+  __shared__ double sb[kKt][kLds];
   __shared__ unsigned long long sm[kTile];
   __shared__ unsigned long long smt[kTile];
-  if (blockIdx.x < blockIdx.y) return;  // symmetric: upper-triangle tiles only
+  // symmetric: only the upper-triangle tiles are launched, XCD-contiguous
+  int64_t ty, tx;
+  if (!tri_tile(blockIdx.x, gridDim.x, gp / kTile, &ty, &tx)) return;
   const int t = threadIdx.x;
   const int lane = t & 63, w = t >> 6;
   const int wr = (w >> 1) * 32, wc = (w & 1) * 32;
-  const int64_t r0 = (int64_t)blockIdx.y * kTile, c0 = (int64_t)blockIdx.x * kTile;
+  const int64_t r0 = ty * kTile, c0 = tx * kTile;
   if (t < kTile) {
     sm[t] = 0ull;
     smt[t] = 0ull;
@@ -143,8 +173,11 @@ __global__ __launch_bounds__(256) void k_coexpr_mask_mfma(const double* __restri
     }
     __syncthreads();
   }
-  // one bit per (row, col) and, off the diagonal, per (col, row)
-  const bool offdiag = blockIdx.x != blockIdx.y;
+  // one bit per (row, col) and, off the diagonal, per (col, row).  A constant
+  // column has z == 0, so its r is exactly 0 and never > thr >= 0: the flags
+  // are only read for a negative threshold.
+  const bool offdiag = tx != ty;
+  const bool chk = thr < 0.0;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -154,7 +187,8 @@ __global__ __launch_bounds__(256) void k_coexpr_mask_mfma(const double* __restri
         const int rl = wr + 16 * i + fk + 4 * q;
         const int cl = wc + 16 * j + fr;
         const int64_t r = r0 + rl, c = c0 + cl;
-        const bool on = r < G && c < G && r != c && !cst[r] && !cst[c] && fabs(acc[i][j][q]) > thr;
+        const bool on = r < G && c < G && r != c && fabs(acc[i][j][q]) > thr &&
+                        !(chk && (cst[r] || cst[c]));
         if (on) {
           atomicOr(&sm[rl], 1ull << cl);
           if (offdiag) atomicOr(&smt[cl], 1ull << rl);
@@ -162,8 +196,8 @@ __global__ __launch_bounds__(256) void k_coexpr_mask_mfma(const double* __restri
       }
   __syncthreads();
   if (t < kTile) {
-    mask[(r0 + t) * (gp / kTile) + blockIdx.x] = sm[t];
-    if (offdiag) mask[(c0 + t) * (gp / kTile) + blockIdx.y] = smt[t];
+    mask[(r0 + t) * (gp / kTile) + tx] = sm[t];
+    if (offdiag) mask[(c0 + t) * (gp / kTile) + ty] = smt[t];
   }
 }
 
@@ -243,6 +277,17 @@ struct DevBuf {
   }
 };
 
+// device timings of the calling thread's last g2v_coexpr_pairs call (ms)
+thread_local double t_mask_ms = 0.0, t_total_ms = 0.0;
+
+struct Events {
+  hipEvent_t e[4] = {nullptr, nullptr, nullptr, nullptr};
+  ~Events() {
+    for (hipEvent_t x : e)
+      if (x) (void)hipEventDestroy(x);
+  }
+};
+
 }  // namespace
 
 #define CX_CHK(x)                                                                   \
@@ -274,11 +319,16 @@ extern "C" int g2v_coexpr_pairs(int device, const double* x, int64_t n_samples, 
                 o_n = o_m + al(8 * gp * words), o_off = o_n + al(8 * gp),
                 o_c = o_off + al(8 * (gp + 1)), ws_bytes = o_c + al(G);
   DevBuf ws, dp;
+  Events ev;
   hipStream_t st = nullptr;
   int64_t total = 0;
+  float ms = 0.f;
+  t_mask_ms = t_total_ms = 0.0;
   CX_CHK(hipSetDevice(device));
   CX_CHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  for (hipEvent_t& e : ev.e) CX_CHK(hipEventCreate(&e));
   CX_CHK(hipMalloc(&ws.p, (size_t)ws_bytes));
+  CX_CHK(hipEventRecord(ev.e[0], st));
   {
     char* base = (char*)ws.p;
     double* dx = (double*)(base + o_x);
@@ -292,9 +342,12 @@ extern "C" int g2v_coexpr_pairs(int device, const double* x, int64_t n_samples, 
     hipLaunchKernelGGL(k_coexpr_stats, dim3((unsigned)((G + 255) / 256)), dim3(256), 0, st,
                        (const double*)dx, n, G, gp, dz, dc);
     CX_CHK(hipGetLastError());
-    hipLaunchKernelGGL(k_coexpr_mask_mfma, dim3((unsigned)words, (unsigned)words), dim3(256), 0,
+    CX_CHK(hipEventRecord(ev.e[1], st));
+    const int64_t tiles = words * (words + 1) / 2;
+    hipLaunchKernelGGL(k_coexpr_mask_mfma, dim3((unsigned)((tiles + 7) / 8 * 8)), dim3(256), 0,
                        st, (const double*)dz, npad, gp, G, (const uint8_t*)dc, threshold, dm);
     CX_CHK(hipGetLastError());
+    CX_CHK(hipEventRecord(ev.e[2], st));
     hipLaunchKernelGGL(k_coexpr_count, dim3((unsigned)((gp + 3) / 4)), dim3(256), 0, st,
                        (const uint64_t*)dm, gp, dn);
     CX_CHK(hipGetLastError());
@@ -317,7 +370,20 @@ extern "C" int g2v_coexpr_pairs(int device, const double* x, int64_t n_samples, 
     rc = g2v::set_error(G2V_ERANGE, "g2v_coexpr_pairs: capacity " + std::to_string(cap) + " < " +
                                         std::to_string(total) + " pairs (*n_pairs holds the count)");
   }
+  CX_CHK(hipEventRecord(ev.e[3], st));
+  CX_CHK(hipEventSynchronize(ev.e[3]));
+  CX_CHK(hipEventElapsedTime(&ms, ev.e[1], ev.e[2]));
+  t_mask_ms = ms;
+  CX_CHK(hipEventElapsedTime(&ms, ev.e[0], ev.e[3]));
+  t_total_ms = ms;
 done:
   if (st) (void)hipStreamDestroy(st);
   return rc;
+}
+
+extern "C" int g2v_coexpr_last_timing(double* mask_ms, double* total_ms) {
+  if (!mask_ms || !total_ms) return g2v::set_error(G2V_EINVAL, "g2v_coexpr_last_timing: null output");
+  *mask_ms = t_mask_ms;
+  *total_ms = t_total_ms;
+  return G2V_OK;
 }

@@ -17,10 +17,13 @@ on the GPU through libg2v.so.
 from __future__ import annotations
 
 import argparse
+import contextlib
 import datetime
+import json
 import logging
 import os
 import random
+import time
 import zlib
 
 from . import generateMatrix as gM
@@ -63,6 +66,21 @@ def _vocab_ids(model, corpus):
                     dtype=np.int32)
 
 
+class _Phases:
+    """wall seconds per CLI phase, summed over iterations (``--timing``)"""
+
+    def __init__(self):
+        self.t = {}
+
+    @contextlib.contextmanager
+    def __call__(self, name):
+        t0 = time.perf_counter()
+        try:
+            yield
+        finally:
+            self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - t0
+
+
 def main(argv=None):
     parser = argparse.ArgumentParser(
         description="Please specify data directory, embedding output directory and data file "
@@ -87,32 +105,37 @@ def main(argv=None):
     parser.add_argument("--no-txt", action="store_true")
     parser.add_argument("--no-w2v", action="store_true")
     parser.add_argument("--w2v-binary", action="store_true")
+    parser.add_argument("--timing", default=None,
+                        help="write wall seconds per phase (summed over iterations) as JSON")
     args = parser.parse_args(argv)
+    ph = _Phases()
     source_dir, export_dir, ending_pattern = args.fileAddress[:3]
 
     logging.basicConfig(format="%(asctime)s : %(levelname)s : %(message)s", level=logging.INFO)
     print("start!")
     rng = random.Random(args.shuffle_seed) if args.shuffle_seed is not None else random
     corpus = None
-    if args.native_ingest:
-        files = os.listdir(source_dir)
-        rng.shuffle(files)
-        paths = [os.path.join(source_dir, f) for f in files if f.endswith(ending_pattern)]
-        print(datetime.datetime.now())
-        print(f"native ingest of {len(paths)} files")
-        corpus = ingest.read_corpus(paths)
-        n_pairs = corpus.n_sent
-    else:
-        gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
-        n_pairs = len(gene_pairs)
+    with ph("ingest"):
+        if args.native_ingest:
+            files = os.listdir(source_dir)
+            rng.shuffle(files)
+            paths = [os.path.join(source_dir, f) for f in files if f.endswith(ending_pattern)]
+            print(datetime.datetime.now())
+            print(f"native ingest of {len(paths)} files")
+            corpus = ingest.read_corpus(paths)
+            n_pairs = corpus.n_sent
+        else:
+            gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
+            n_pairs = len(gene_pairs)
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
     perm_buf = None
-    if corpus is not None:
-        perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng)
-        corpus.permute_(perm_buf)
-    else:
-        rng.shuffle(gene_pairs)
+    with ph("shuffle"):
+        if corpus is not None:
+            perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng)
+            corpus.permute_(perm_buf)
+        else:
+            rng.shuffle(gene_pairs)
     print(datetime.datetime.now())
     print("shuffle done " + str(n_pairs))
 
@@ -128,44 +151,59 @@ def main(argv=None):
         if current_iter == 1:
             print(f"gene2vec dimension {dimension} iteration {current_iter} start")
             if corpus is None:
-                model = Word2Vec(gene_pairs, **kw)
+                with ph("train"):
+                    model = Word2Vec(gene_pairs, **kw)
             else:
-                model = Word2Vec(**kw)
-                model._build_from_counts(corpus.vocab_raw_counts())
-                model.corpus_count = corpus.n_sent
-                model.corpus_total_words = int(corpus.sent_off[-1])
-                ids = _vocab_ids(model, corpus)
-                model.train_ids(ids[corpus.tokens], corpus.sent_off,
-                                total_examples=model.corpus_count, epochs=model.iter)
+                with ph("vocab"):
+                    model = Word2Vec(**kw)
+                    model._build_from_counts(corpus.vocab_raw_counts())
+                    model.corpus_count = corpus.n_sent
+                    model.corpus_total_words = int(corpus.sent_off[-1])
+                    ids = _vocab_ids(model, corpus)
+                    tok = ids[corpus.tokens]
+                with ph("train"):
+                    model.train_ids(tok, corpus.sent_off,
+                                    total_examples=model.corpus_count, epochs=model.iter)
         else:
             print(datetime.datetime.now())
             print("shuffle start " + str(n_pairs))
-            if corpus is not None:
-                perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng, out=perm_buf)
-                corpus.permute_(perm_buf)
-            else:
-                rng.shuffle(gene_pairs)
+            with ph("shuffle"):
+                if corpus is not None:
+                    perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng, out=perm_buf)
+                    corpus.permute_(perm_buf)
+                else:
+                    rng.shuffle(gene_pairs)
             print(datetime.datetime.now())
             print("shuffle done " + str(n_pairs))
             print(f"gene2vec dimension {dimension} iteration {current_iter} start")
             prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
-            model = Word2Vec.load(prev, device=args.device)
+            with ph("load"):
+                model = Word2Vec.load(prev, device=args.device)
             if corpus is None:
-                model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
+                with ph("train"):
+                    model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
             else:
-                ids = _vocab_ids(model, corpus)
-                model.train_ids(ids[corpus.tokens], corpus.sent_off,
-                                total_examples=model.corpus_count, epochs=model.iter)
-        model.save(name)
-        if not args.no_txt:
-            gM.outputTxt(name)
-        if not args.no_w2v:
-            model.wv.save_word2vec_format(name + "_w2v.txt", binary=False)
-            if args.w2v_binary:
-                model.wv.save_word2vec_format(name + "_w2v.bin", binary=True)
+                with ph("vocab"):
+                    tok = _vocab_ids(model, corpus)[corpus.tokens]
+                with ph("train"):
+                    model.train_ids(tok, corpus.sent_off,
+                                    total_examples=model.corpus_count, epochs=model.iter)
+        with ph("save"):
+            model.save(name)
+        with ph("txt"):
+            if not args.no_txt:
+                gM.outputTxt(name)
+        with ph("w2v"):
+            if not args.no_w2v:
+                model.wv.save_word2vec_format(name + "_w2v.txt", binary=False)
+                if args.w2v_binary:
+                    model.wv.save_word2vec_format(name + "_w2v.bin", binary=True)
         print(f"gene2vec dimension {dimension} iteration {current_iter} done")
         outputs.append(name)
         del model
+    if args.timing:
+        with open(args.timing, "w") as f:
+            json.dump({k: round(v, 4) for k, v in ph.t.items()}, f)
     return outputs
 
 

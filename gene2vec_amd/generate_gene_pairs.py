@@ -60,6 +60,14 @@ def coexpr_indices(values: np.ndarray, corr_threshold: float, device: int = 0) -
     return out[:cnt.value]
 
 
+def last_timing() -> tuple:
+    """(fused correlation kernel ms, whole call ms) of this thread's last
+    ``coexpr_indices`` call, from HIP events on its stream."""
+    m, t = C.c_double(0), C.c_double(0)
+    N.check(N.lib().g2v_coexpr_last_timing(C.byref(m), C.byref(t)))
+    return m.value, t.value
+
+
 def coexpr(data, corr_threshold: float | None = None, device: int = 0) -> list:
     """``src/generate_gene_pairs.py:45-65``: "name_a name_b" strings."""
     thr = CORR_THRESHOLD if corr_threshold is None else corr_threshold

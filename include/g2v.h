@@ -211,6 +211,10 @@ int g2v_format_f32(const float *x, int64_t n, char *out, int64_t cap, int64_t *w
  * synchronises. */
 int g2v_coexpr_pairs(int device, const double *x, int64_t n_samples, int64_t n_genes,
                      double threshold, int32_t *pairs, int64_t cap, int64_t *n_pairs);
+/* Device time of the calling thread's last g2v_coexpr_pairs call, from HIP
+ * events on its stream: the fused correlation+threshold kernel alone and the
+ * whole call (H2D copy .. D2H of the pairs).  Zero before any call. */
+int g2v_coexpr_last_timing(double *mask_ms, double *total_ms);
 
 /* ---- consumer side ----------------------------------------------------------------- */
 /* gensim wv.similarity for n index pairs (src/evaluation_target_function.py:38,49):

@@ -43,6 +43,7 @@ def write_corpus(d, pairs, n_files, names, tag="pairs"):
             f.write("\n".join(lines.tolist()))
             f.write("\n")
         sizes.append(os.path.getsize(path))
+        print(f"wrote {path} ({sizes[-1]} B)", flush=True)
     return sum(sizes)
 
 

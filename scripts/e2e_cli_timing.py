@@ -56,14 +56,16 @@ def main():
     t = time.perf_counter()
     with contextlib.redirect_stdout(log):
         outs = G.main([data, out, "txt", "--native-ingest", "--hash", "crc32",
-                       "--shuffle-seed", "7", "--iters", str(a.iters)])
+                       "--shuffle-seed", "7", "--iters", str(a.iters),
+                       "--timing", os.path.join(work, "phases.json")])
     total = time.perf_counter() - t
     sizes = {os.path.basename(f): os.path.getsize(f) for f in
              [outs[-1] + ".txt", outs[-1] + "_w2v.txt"]}
     res = {"metric": "gene2vec CLI end to end (native ingest + %d iterations + exports)" % a.iters,
            "pairs": a.pairs, "files": a.files, "wall_s": round(total, 2),
            "pairs_per_s_incl_io": round(a.pairs * a.iters / total, 1),
-           "corpus_write_s_excluded": round(t_write, 2), "outputs": sizes}
+           "corpus_write_s_excluded": round(t_write, 2), "outputs": sizes,
+           "phases_s": json.load(open(os.path.join(work, "phases.json")))}
     print(json.dumps(res))
     if not a.keep:
         shutil.rmtree(work, ignore_errors=True)
