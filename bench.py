@@ -64,6 +64,9 @@ def parse():
                    help="skip the (untimed) write-free gather-roof measurement")
     p.add_argument("--dist", action="store_true",
                    help="init torch.distributed (RCCL) and average replicas even at N=1")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                   help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
+                        "the N>1 path with several ranks sharing one GPU)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return p.parse_args()
 
@@ -81,6 +84,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.backend == "gloo":
+        # rehearsal mode: ranks beyond the visible GPUs share them round-robin
+        local %= max(1, torch.cuda.device_count())
     use_dist = world > 1 or a.dist
     if use_dist:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
@@ -89,7 +95,10 @@ def main():
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if a.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
     n_pairs = a.pairs or (100_000_000 if world == 1 else 125_000_000)
     V0, D, K = a.vocab, a.dim, a.negative
