@@ -36,7 +36,7 @@ BATCH_WORDS = 10000
 MAX_DIM = 512
 TXT_MATRIX = 0
 TXT_W2V = 1
-SUPPORTED_NEGATIVE = (1, 2, 3, 5, 10, 15, 20)
+SUPPORTED_NEGATIVE = tuple(range(1, 21))
 
 
 class NativeLibraryError(RuntimeError):

@@ -15,7 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libg2v.so")
-K_COMPILED = (1, 2, 3, 5, 10, 15, 20)  # == G2V_FOR_EACH_K in g2v_internal.h
+K_COMPILED = tuple(range(1, 21))  # == G2V_FOR_EACH_K in g2v_internal.h
 # (source, extra defines, object name): the SGNS kernels are built once per K
 UNITS = ([("g2v_sgns_atomic.hip", [f"-DG2V_K={k}"], f"g2v_sgns_atomic_k{k}.o") for k in K_COMPILED]
          + [("g2v_sgns.hip", [f"-DG2V_K={k}"], f"g2v_sgns_k{k}.o") for k in K_COMPILED]

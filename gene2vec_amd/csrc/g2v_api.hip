@@ -199,7 +199,7 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
   const int nvec = (vector_size + 3) / 4;
   const int nv = nvec <= 64 ? 1 : 2;
   REQUIRE(sgns_supported(negative, nv), G2V_EINVAL,
-          "negative=%d not compiled (supported: 1,2,3,5,10,15,20)", negative);
+          "negative=%d not compiled (supported: 1..20)", negative);
   // the update kernels address a table through one buffer resource (32-bit offsets)
   REQUIRE((int64_t)vocab_size * ((vector_size + 31) / 32 * 32) * 4 < ((int64_t)1 << 31),
           G2V_EINVAL, "vocab_size=%d x vector_size=%d exceeds the 2 GiB per-table limit",

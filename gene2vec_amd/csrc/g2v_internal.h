@@ -94,7 +94,9 @@ hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
 // negative counts compiled into the SGNS kernels; g2v_sgns.hip and
 // g2v_sgns_atomic.hip are built once per K (-DG2V_K=K) and define the per-K
 // entry points below; the dispatchers live in g2v_kernels.hip
-#define G2V_FOR_EACH_K(X) X(1) X(2) X(3) X(5) X(10) X(15) X(20)
+#define G2V_FOR_EACH_K(X)                                                                  \
+  X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16)  \
+  X(17) X(18) X(19) X(20)
 #define G2V_DECL_K(KK)                                                                     \
   hipError_t launch_sgns_k##KK(const SgnsArgs& a, int nv, int mode, int pol, int grid,     \
                                hipStream_t st);                                            \

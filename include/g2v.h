@@ -81,7 +81,7 @@ int g2v_abi_version(void);
 /* Replaces gensim's Word2Vec(size=vector_size, window, negative, hs=0, sg=1)
  * model state ([ext] BaseWordEmbeddingsModel.__init__; src/gene2vec.py:70).
  * window must be 1 (src/gene2vec.py:62); negative in the compiled set
- * {1,2,3,5,10,15,20}; 1 <= vector_size <= G2V_MAX_DIM. */
+ * 1..20; 1 <= vector_size <= G2V_MAX_DIM. */
 int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t negative,
                int32_t window, g2v_ctx **out);
 int g2v_destroy(g2v_ctx *ctx);

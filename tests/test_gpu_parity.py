@@ -98,7 +98,7 @@ def test_sampler_reference_corpus(test_pairs, sample):
     assert got.tolist() == [[c, j] + n for c, j, n in ref2]
 
 
-@pytest.mark.parametrize("K", [5, 15])
+@pytest.mark.parametrize("K", [5, 15, 7, 20])
 @pytest.mark.parametrize("sample", [0.0, 1e-3, 1e-5])
 def test_sampler_zipf_pairs(K, sample):
     pairs = zipf_pairs(60000, 3000, seed=5)
@@ -142,7 +142,7 @@ def test_step_sequential_golden(name):
 
 
 @pytest.mark.parametrize("D,K", [(200, 5), (512, 15), (100, 5), (50, 3), (7, 1), (256, 20),
-                                 (300, 10), (64, 2)])
+                                 (300, 10), (64, 2), (200, 4), (128, 7), (333, 12), (512, 19)])
 def test_step_sequential_vs_c_oracle(D, K):
     rng = np.random.Generator(np.random.PCG64(D * 100 + K))
     V, B = 37, 500  # small V: many repeated rows and repeated negatives
@@ -163,7 +163,7 @@ def test_step_sequential_vs_c_oracle(D, K):
 
 
 @pytest.mark.parametrize("D,K", [(200, 5), (512, 15), (7, 1), (64, 2), (100, 3), (300, 10),
-                                 (256, 20), (508, 5)])
+                                 (256, 20), (508, 5), (200, 4), (150, 8), (260, 13), (512, 18)])
 def test_step_hogwild_disjoint_equals_sequential(D, K):
     """examples touching disjoint rows: every update order gives the same
     result -- the production atomic kernel for every compiled negative count,

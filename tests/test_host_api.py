@@ -38,7 +38,7 @@ def test_vocab_and_init_match_oracle(test_pairs, golden):
 
 
 def test_unsupported_configs_raise():
-    for kw in (dict(sg=0), dict(sg=1, hs=1), dict(sg=1, window=5), dict(sg=1, negative=4),
+    for kw in (dict(sg=0), dict(sg=1, hs=1), dict(sg=1, window=5), dict(sg=1, negative=21), dict(sg=1, negative=0),
                dict(sg=1, size=1000)):
         with pytest.raises(NotImplementedError):
             Word2Vec(**kw)

@@ -38,7 +38,7 @@ def test_error_path_without_gpu_is_loud():
     rc = N.lib().g2v_create(0, 10, 8, 5, 2, C.byref(h))  # window=2 rejected up front
     assert rc == N.G2V_EINVAL
     assert b"window" in N.lib().g2v_last_error()
-    rc = N.lib().g2v_create(0, 10, 8, 4, 1, C.byref(h))  # negative=4 not compiled
+    rc = N.lib().g2v_create(0, 10, 8, 21, 1, C.byref(h))  # negative=21 not compiled
     assert rc == N.G2V_EINVAL
     rc = N.lib().g2v_create(0, 10, 513, 5, 1, C.byref(h))  # wider than one wave's 2 float4s
     assert rc == N.G2V_EINVAL
