@@ -102,6 +102,8 @@ struct g2v_ctx {
   int stripe_rows = 8, stripe_copies = 8;
   float* stripe = nullptr;
   int64_t stripe_cap = 0;
+  uint32_t* dbg16 = nullptr;  // ablation 3: packed-f16 atomic scratch [2][V + stripes][ld/2]
+  int64_t dbg16_cap = 0;
   hipStream_t own_stream = nullptr, stream = nullptr;
 
   float *own0 = nullptr, *own1 = nullptr;  // context-owned tables
@@ -305,6 +307,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->snap1);
   dev_free(c->d_counters);
   dev_free(c->stripe);
+  dev_free(c->dbg16);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
@@ -368,7 +371,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_copies = (int)value;
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 2, G2V_EINVAL, "debug write mode out of [0, 2]");
+      REQUIRE(value >= 0 && value <= 3, G2V_EINVAL, "debug write mode out of [0, 3]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_GRID:
@@ -649,6 +652,12 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     }
   }
   s.stripe = c->stripe;
+  if (c->debug_write == 3) {
+    const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
+    if ((rc = dev_reserve(c->stream, &c->dbg16, &c->dbg16_cap, rows * c->ld))) return rc;
+    HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
+  }
+  s.dbg16 = c->dbg16;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timing) {
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;

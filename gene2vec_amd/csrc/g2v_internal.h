@@ -76,13 +76,15 @@ struct SgnsArgs {
   int D;
   int V;
   int hot_rows;             // rows [0, hot_rows) are updated with float atomics
-  int debug_write;          // ablation: 0 atomics, 1 plain stores, 2 no writes
+  int debug_write;          // ablation: 0 atomics, 1 plain stores, 2 no writes,
+                            // 3 packed-f16 atomics into a scratch table
   const float* exp_table;   // [1000]
   // hot-row striping (k_sgns_atomic): rows [0, stripe_rows) of each table have
   // stripe_copies-1 extra copies; value = main + sum(copies), atomics spread
   float* stripe;            // [2][stripe_copies-1][stripe_rows][ld]
   int stripe_rows;
   int stripe_copies;        // 1 = off
+  uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]
 };
 
 hipError_t launch_job_sample(bool write, const SampleArgs& a, int64_t n_jobs, hipStream_t st);

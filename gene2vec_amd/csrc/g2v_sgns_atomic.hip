@@ -90,7 +90,8 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 }
 
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
-// 2 no table writes
+// 2 no table writes, 3 packed-f16 atomics into a scratch table (half the atomic
+// bytes, tables never written: a throughput probe)
 template <int WR>
 __device__ __forceinline__ void upd(float* p, float v) {
   if (WR == 0) atomicAdd(p, v);
@@ -207,6 +208,33 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 
       // ---- atomics of example e -----------------------------------------------
       const int cbase = (int)(e % (int64_t)a.stripe_copies);
+      if (WR == 3) {
+        typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+        const int hw = (int)(a.ld >> 1);
+        const int n2 = (D + 1) >> 1;  // half2 words per row
+        const int64_t nrow = (int64_t)a.V + (int64_t)(a.stripe_copies - 1) * a.stripe_rows;
+#pragma unroll
+        for (int d = 0; d <= NT; ++d) {
+          const bool w = d == NT;
+          const float cf = w ? (any ? lf : 0.f) : g[d];
+          if (cf == 0.f) continue;
+          const int t = w ? input : tg[d];
+          // hot rows keep their stripe copies: copy c of row t lives at V + (c-1)*rows + t
+          const int cc = (cbase + d) % a.stripe_copies;
+          const int64_t rr = (cc == 0 || t >= a.stripe_rows)
+                                 ? t : a.V + (int64_t)(cc - 1) * a.stripe_rows + t;
+          uint32_t* row = a.dbg16 + ((w ? 0 : 1) * nrow + rr) * hw;
+          const float* src = w ? sw : s1;
+          for (int i = lane; i < n2; i += 64) {
+            h2_t v;
+            v.x = (_Float16)(cf * src[2 * i]);
+            v.y = (_Float16)(cf * src[2 * i + 1]);
+            __builtin_amdgcn_global_atomic_fadd_v2f16(reinterpret_cast<h2_t*>(row + i), v);
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        continue;
+      }
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         if (g[d] == 0.f) continue;
@@ -265,6 +293,10 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 2) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 3) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 3>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
 #endif
