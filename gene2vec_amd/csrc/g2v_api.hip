@@ -371,7 +371,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_copies = (int)value;
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 3, G2V_EINVAL, "debug write mode out of [0, 3]");
+      REQUIRE(value >= 0 && value <= 4, G2V_EINVAL, "debug write mode out of [0, 4]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_GRID:
@@ -652,9 +652,10 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     }
   }
   s.stripe = c->stripe;
-  if (c->debug_write == 3) {
+  if (c->debug_write >= 3) {
     const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
-    if ((rc = dev_reserve(c->stream, &c->dbg16, &c->dbg16_cap, rows * c->ld))) return rc;
+    const int64_t words = rows * c->ld * (c->debug_write == 4 ? 2 : 1);
+    if ((rc = dev_reserve(c->stream, &c->dbg16, &c->dbg16_cap, words))) return rc;
     HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
   }
   s.dbg16 = c->dbg16;

@@ -61,7 +61,15 @@ __device__ __forceinline__ void load_row(float4 (&o)[NV], const SgnsArgs& a,
 }
 
 // destination of an atomic delta for row t of table tbl: main or stripe copy c
+// (WR 4, ablation: the same rows of a scratch table the kernel never reads)
+template <int WR = 0>
 __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int c) {
+  if (WR == 4) {
+    const int64_t nrow = (int64_t)a.V + (int64_t)(a.stripe_copies - 1) * a.stripe_rows;
+    const int64_t rr =
+        (c == 0 || t >= a.stripe_rows) ? t : a.V + (int64_t)(c - 1) * a.stripe_rows + t;
+    return reinterpret_cast<float*>(a.dbg16) + (tbl * nrow + rr) * a.ld;
+  }
   if (c == 0 || t >= a.stripe_rows) return (tbl ? a.wr1 : a.wr0) + (int64_t)t * a.ld;
   return a.stripe + (((int64_t)tbl * (a.stripe_copies - 1) + (c - 1)) * a.stripe_rows + t) * a.ld;
 }
@@ -91,10 +99,11 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
 // 2 no table writes, 3 packed-f16 atomics into a scratch table (half the atomic
-// bytes, tables never written: a throughput probe)
+// bytes, tables never written: a throughput probe), 4 the production f32
+// atomics into that scratch table (tables never written)
 template <int WR>
 __device__ __forceinline__ void upd(float* p, float v) {
-  if (WR == 0) atomicAdd(p, v);
+  if (WR == 0 || WR == 4) atomicAdd(p, v);
   else if (WR == 1) *p = v;
 }
 
@@ -238,11 +247,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         if (g[d] == 0.f) continue;
-        float* row = upd_row(a, 1, tg[d], (cbase + d) % a.stripe_copies) + lane;
+        float* row = upd_row<WR>(a, 1, tg[d], (cbase + d) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, g[d] * s1[64 * i + lane]);
       }
       if (any) {
-        float* row = upd_row(a, 0, input, (cbase + NT) % a.stripe_copies) + lane;
+        float* row = upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, lf * sw[64 * i + lane]);
       }
       if (tail && any) {
@@ -266,7 +275,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           }
           if (lane / tail < tpack && q <= NT && coef != 0.f) {
             const float src = from_work ? sw[el] : s1[el];
-            float* row = upd_row(a, from_work ? 0 : 1, row_t, (cbase + q) % a.stripe_copies);
+            float* row = upd_row<WR>(a, from_work ? 0 : 1, row_t, (cbase + q) % a.stripe_copies);
             upd<WR>(row + el, coef * src);
           }
         }
@@ -293,6 +302,10 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 2) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 4) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 4>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
   if (nv == 1 && a.debug_write == 3) {
