@@ -107,12 +107,24 @@ def main(argv=None):
     parser.add_argument("--w2v-binary", action="store_true")
     parser.add_argument("--timing", default=None,
                         help="write wall seconds per phase (summed over iterations) as JSON")
+    parser.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
+                        help="data-parallel process group under torchrun (nccl = RCCL over "
+                             "xGMI; gloo only to rehearse with ranks sharing a GPU)")
+    parser.add_argument("--merge-every-jobs", type=int, default=1024,
+                        help="data-parallel replica merge cadence (gensim jobs per rank)")
     args = parser.parse_args(argv)
+    rank, world = _init_dp(args)
     ph = _Phases()
     source_dir, export_dir, ending_pattern = args.fileAddress[:3]
 
     logging.basicConfig(format="%(asctime)s : %(levelname)s : %(message)s", level=logging.INFO)
     print("start!")
+    if world > 1 and args.shuffle_seed is None:
+        # every rank must shuffle identically: rank 0 draws the seed
+        import torch.distributed as dist
+        box = [random.randrange(2 ** 63) if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        args.shuffle_seed = box[0]
     rng = random.Random(args.shuffle_seed) if args.shuffle_seed is not None else random
     corpus = None
     with ph("ingest"):
@@ -146,6 +158,8 @@ def main(argv=None):
     kw = dict(size=dimension, window=args.window, min_count=1, workers=args.workers, iter=1, sg=1,
               negative=args.negative, sample=args.sample, hashfxn=hashfxn, device=args.device,
               mode=args.mode)
+    import gene2vec_amd.word2vec as W
+    W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
     for current_iter in range(1, args.iters + 1):
         name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
         if current_iter == 1:
@@ -189,22 +203,55 @@ def main(argv=None):
                     model.train_ids(tok, corpus.sent_off,
                                     total_examples=model.corpus_count, epochs=model.iter)
         with ph("save"):
-            model.save(name)
+            model._sync_host()
+            if rank == 0:  # data parallel: the merged replicas are identical
+                model.save(name)
         with ph("txt"):
-            if not args.no_txt:
+            if not args.no_txt and rank == 0:
                 gM.outputTxt(name)
         with ph("w2v"):
-            if not args.no_w2v:
+            if not args.no_w2v and rank == 0:
                 model.wv.save_word2vec_format(name + "_w2v.txt", binary=False)
                 if args.w2v_binary:
                     model.wv.save_word2vec_format(name + "_w2v.bin", binary=True)
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()  # the next iteration loads rank 0's checkpoint
         print(f"gene2vec dimension {dimension} iteration {current_iter} done")
         outputs.append(name)
         del model
-    if args.timing:
+    if args.timing and rank == 0:
         with open(args.timing, "w") as f:
             json.dump({k: round(v, 4) for k, v in ph.t.items()}, f)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return outputs
+
+
+def _init_dp(args):
+    """torchrun launch (WORLD_SIZE > 1): one rank per GPU, the pair file
+    shared and sharded by Word2Vec.train_ids, replicas merged over RCCL.
+    Returns (rank, world)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
+        return 0, 1
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.backend == "gloo":
+        local %= max(1, torch.cuda.device_count())
+    args.device = local
+    torch.cuda.set_device(local)
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
+    # Python's per-process hash() seeds a different init on every rank: harmless,
+    # Word2Vec broadcasts rank 0's tables before training
+    return rank, world
 
 
 if __name__ == "__main__":

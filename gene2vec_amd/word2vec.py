@@ -27,6 +27,7 @@ import zipfile
 import numpy as np
 
 from . import _native as N
+from . import distributed as Dd
 from . import engine as E
 
 logger = logging.getLogger(__name__)
@@ -290,6 +291,10 @@ def _load_npz(fname):
 # ---------------------------------------------------------------------------
 # Word2Vec
 # ---------------------------------------------------------------------------
+# replica merge cadence for data-parallel training (gensim jobs per rank)
+DP_MERGE_EVERY_JOBS = 1024
+
+
 class Word2Vec:
     """Skip-gram negative-sampling Word2Vec trained on an MI355X.
 
@@ -340,6 +345,7 @@ class Word2Vec:
         self.callbacks = callbacks
         self.device = device
         self.mode = mode
+        self.merge_every_jobs = DP_MERGE_EVERY_JOBS
         self.random = np.random.RandomState(seed)
         self.corpus_count = 0
         self.corpus_total_words = 0
@@ -352,6 +358,7 @@ class Word2Vec:
         self.cum_table = None
         self.last_stats = None
         self._engine = None
+        self._replica = None
         self._dev_dirty = False  # device tables newer than host copies
         if sentences is not None:
             self.build_vocab(sentences)
@@ -401,7 +408,42 @@ class Word2Vec:
         if self._engine is not None:
             self._engine.close()
         self._engine = None
+        self._replica = None
         self._dev_dirty = False
+
+    @staticmethod
+    def _dp_world():
+        """(rank, world) of an initialised torch.distributed group, else (0, 1)."""
+        try:
+            import torch.distributed as dist
+        except ImportError:  # pragma: no cover
+            return 0, 1
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
+
+    def _bind_replica(self, eng):
+        """Data-parallel replica (no reference equivalent: gensim is one process,
+        src/gene2vec.py:59): both tables in one torch-owned [2][V][ld] device
+        buffer bound into the engine, rank 0's values broadcast (Python's hash()
+        seeds the init differently in every process), and one ReplicaTrainer
+        merging the replicas row-wise every ``merge_every_jobs`` jobs over the
+        process group (RCCL over xGMI with backend "nccl")."""
+        import torch
+        import torch.distributed as dist
+        dev = torch.device("cuda", self.device)
+        # engine launches, merges and collectives ordered on one non-default stream
+        stream = torch.cuda.Stream(dev)
+        torch.cuda.set_stream(stream)
+        eng.set_stream(stream.cuda_stream)
+        V, D = len(self.wv.index2word), self.vector_size
+        tables = torch.zeros((2, V, eng.ld), dtype=torch.float32, device=dev)
+        tables[0, :, :D] = torch.from_numpy(np.ascontiguousarray(self.wv.vectors)).to(dev)
+        tables[1, :, :D] = torch.from_numpy(np.ascontiguousarray(self.syn1neg)).to(dev)
+        dist.broadcast(tables, src=0)
+        eng.bind_tables(tables[0].data_ptr(), tables[1].data_ptr(), eng.ld, keepalive=(tables,))
+        mode = N.MODE_SEQUENTIAL if self.mode == "sequential" else N.MODE_HOGWILD
+        self._replica = Dd.ReplicaTrainer(eng, (tables,), self.merge_every_jobs, mode)
 
     def _ensure_engine(self):
         if self._engine is not None:
@@ -417,6 +459,9 @@ class Word2Vec:
         if not np.array_equal(si, expect):
             raise RuntimeError("device sample_int differs from the host vocabulary")
         eng.set_weights(wv.vectors, self.syn1neg, self.vectors_lockf)
+        self._replica = None
+        if self._dp_world()[1] > 1:
+            self._bind_replica(eng)
         self._engine = eng
         return eng
 
@@ -463,6 +508,20 @@ class Word2Vec:
         self.min_alpha = float(end_alpha or self.min_alpha)
         self.epochs = epochs
         eng = self._ensure_engine()
+        rank, world = self._dp_world()
+        if world > 1:
+            # contiguous shard of the (shuffled) sentences per rank; alpha follows
+            # the shard's own progress, which is the global progress (all ranks
+            # advance together)
+            n_all = len(tokens) // sent_len if sent_len > 0 else len(sent_off) - 1
+            s0, s1 = Dd.shard_range(n_all, rank, world)
+            if sent_len > 0:
+                tokens = tokens[s0 * sent_len:s1 * sent_len]
+            else:
+                so = np.asarray(sent_off, dtype=np.int64)
+                tokens = tokens[so[s0]:so[s1]]
+                sent_off = so[s0:s1 + 1] - so[s0]
+            total_examples, total_words = s1 - s0, None
         if sent_len > 0:
             n_sent = len(tokens) // sent_len
             eng.set_corpus(tokens, sent_len=sent_len)
@@ -494,8 +553,16 @@ class Word2Vec:
                 prog = (cur_epoch + pushed[1:] / total) / epochs
                 al[1:] = np.maximum(self.min_alpha,
                                     self.alpha - (self.alpha - self.min_alpha) * prog)
-            seeds = E.job_seeds(self.random, len(js) - 1)
-            eng.train(js, al, seeds, mode)
+            if world > 1:
+                # every rank draws the same base from model.random (kept in step
+                # across ranks), then a stream of its own
+                base = int(self.random.randint(0, 2 ** 31 - 1))
+                seeds = E.job_seeds(np.random.RandomState((base + 7919 * rank) % 2 ** 32),
+                                    len(js) - 1)
+                self._replica.train_epoch(js, al, seeds)
+            else:
+                seeds = E.job_seeds(self.random, len(js) - 1)
+                eng.train(js, al, seeds, mode)
             st = eng.read_stats()
             stats.append(st)
             if len(al):
@@ -564,6 +631,7 @@ class Word2Vec:
         m.compute_loss = False
         m.callbacks = ()
         m.device = 0
+        m.merge_every_jobs = DP_MERGE_EVERY_JOBS
         m.total_train_time = 0.0
         m.running_training_loss = 0.0
         m.random = np.random.RandomState()
@@ -576,6 +644,7 @@ class Word2Vec:
         m.cum_table = arrs.get("cum_table")
         m.last_stats = None
         m._engine = None
+        m._replica = None
         m._dev_dirty = False
         return m
 
