@@ -858,7 +858,8 @@ int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
   HIPCHK(hipStreamSynchronize(c->stream));
   unsigned long long cnt[4] = {0, 0, 0, 0};
   HIPCHK(hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
-  HIPCHK(hipMemset(c->d_counters, 0, sizeof cnt));
+  HIPCHK(hipMemsetAsync(c->d_counters, 0, sizeof cnt, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
   memset(out, 0, sizeof *out);
   out->effective_words = (int64_t)cnt[0];
   out->examples = (int64_t)cnt[1];

@@ -243,7 +243,10 @@ def _zipf_setup(n_pairs, V, D, K, sample, seed=20250114):
     return tok, counts, syn0
 
 
-def test_train_sequential_vs_c_oracle_zipf():
+@pytest.mark.parametrize("seg_jobs", [0, 3, 1])
+def test_train_sequential_vs_c_oracle_zipf(seg_jobs):
+    """seg_jobs > 0 splits the 8 jobs into segments: segment s+1 is sampled on
+    the side stream into the other workspace while segment s trains"""
     D, K, sample = 200, 5, 1e-3
     tok, counts, syn0 = _zipf_setup(40000, 2000, D, K, sample)
     V = len(counts)
@@ -252,6 +255,8 @@ def test_train_sequential_vs_c_oracle_zipf():
     al = E.job_alphas(js, len(tok) // 2)
     sd = E.job_seeds(np.random.RandomState(1), len(js) - 1)
     eng = E.SGNSEngine(V, D, K)
+    if seg_jobs:
+        eng.set_option(N.OPT_SEG_JOBS, seg_jobs)
     eng.set_vocab(counts, sample)
     eng.set_weights(syn0, np.zeros((V, D), np.float32))
     eng.set_corpus(tok, sent_len=2)
@@ -276,8 +281,8 @@ def _eval_loss(syn0, syn1, tok, counts, K, n_eval=20000, seed=99):
     return O.sgns_loss(syn0, syn1, c, j, negs)
 
 
-@pytest.mark.parametrize("D,K", [(200, 5), (512, 15)])
-def test_train_hogwild_objective_matches_oracle(D, K):
+@pytest.mark.parametrize("D,K,seg_jobs", [(200, 5, 0), (512, 15, 0), (200, 5, 7)])
+def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs):
     """Hogwild GPU vs the sequential oracle on the same jobs/seeds: the SGNS
     objective on held-in pairs must agree within 2 % (Hogwild reorders
     updates; it is judged end-to-end)."""
@@ -287,6 +292,8 @@ def test_train_hogwild_objective_matches_oracle(D, K):
     off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
     js = E.plan_jobs(n_sent=len(tok) // 2, sent_len=2)
     eng = E.SGNSEngine(V, D, K)
+    if seg_jobs:
+        eng.set_option(N.OPT_SEG_JOBS, seg_jobs)  # pipelined sampler/SGNS segments
     eng.set_vocab(counts, sample)
     eng.set_weights(syn0, np.zeros((V, D), np.float32))
     eng.set_corpus(tok, sent_len=2)
