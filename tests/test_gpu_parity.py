@@ -142,7 +142,8 @@ def test_step_sequential_golden(name):
 
 
 @pytest.mark.parametrize("D,K", [(200, 5), (512, 15), (100, 5), (50, 3), (7, 1), (256, 20),
-                                 (300, 10), (64, 2), (200, 4), (128, 7), (333, 12), (512, 19)])
+                                 (300, 10), (64, 2), (200, 4), (128, 7), (333, 12), (512, 19),
+                                 (1, 5), (2, 1), (65, 3)])
 def test_step_sequential_vs_c_oracle(D, K):
     rng = np.random.Generator(np.random.PCG64(D * 100 + K))
     V, B = 37, 500  # small V: many repeated rows and repeated negatives
@@ -163,7 +164,8 @@ def test_step_sequential_vs_c_oracle(D, K):
 
 
 @pytest.mark.parametrize("D,K", [(200, 5), (512, 15), (7, 1), (64, 2), (100, 3), (300, 10),
-                                 (256, 20), (508, 5), (200, 4), (150, 8), (260, 13), (512, 18)])
+                                 (256, 20), (508, 5), (200, 4), (150, 8), (260, 13), (512, 18),
+                                 (1, 2), (65, 6)])
 def test_step_hogwild_disjoint_equals_sequential(D, K):
     """examples touching disjoint rows: every update order gives the same
     result -- the production atomic kernel for every compiled negative count,
@@ -245,8 +247,8 @@ def _zipf_setup(n_pairs, V, D, K, sample, seed=20250114):
 
 @pytest.mark.parametrize("seg_jobs", [0, 3, 1])
 def test_train_sequential_vs_c_oracle_zipf(seg_jobs):
-    """seg_jobs > 0 splits the 8 jobs into segments: segment s+1 is sampled on
-    the side stream into the other workspace while segment s trains"""
+    """seg_jobs > 0 splits the 8 jobs into several sample -> update segments
+    (sampler state, LCG streams and alpha carried across segment boundaries)"""
     D, K, sample = 200, 5, 1e-3
     tok, counts, syn0 = _zipf_setup(40000, 2000, D, K, sample)
     V = len(counts)
@@ -269,6 +271,45 @@ def test_train_sequential_vs_c_oracle_zipf(seg_jobs):
     assert (st["effective_words"], st["examples"]) == (ref["effective_words"], ref["examples"])
     _close(g0, a0, atol=1e-6)
     _close(g1, a1, atol=1e-6)
+
+
+@pytest.mark.parametrize("V", [1, 2, 3])
+@pytest.mark.parametrize("mode", ["sequential", "hogwild"])
+def test_train_tiny_vocabulary(V, mode):
+    """degenerate vocabularies: one gene (every negative equals the center and
+    is skipped), two and three genes; sequential vs the C oracle at 1e-5,
+    Hogwild: identical counts and finite tables"""
+    D, K, sample = 16, 5, 1e-3
+    rng = np.random.RandomState(V)
+    n = 3000
+    pairs = rng.randint(0, V, (n, 2)).astype(np.int32)
+    tok = pairs.reshape(-1)
+    counts = np.bincount(tok, minlength=V).astype(np.int64)
+    order = np.argsort(-counts, kind="stable")
+    remap = np.empty(V, np.int32)
+    remap[order] = np.arange(V, dtype=np.int32)
+    tok = remap[tok]
+    counts = counts[order]
+    syn0 = ((np.random.Generator(np.random.PCG64(2)).random((V, D)) - 0.5) / D).astype(np.float32)
+    off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    al = E.job_alphas(js, n)
+    sd = E.job_seeds(np.random.RandomState(1), len(js) - 1)
+    eng = E.SGNSEngine(V, D, K)
+    eng.set_vocab(counts, sample)
+    eng.set_weights(syn0, np.zeros((V, D), np.float32))
+    eng.set_corpus(tok, sent_len=2)
+    eng.train(js, al, sd, N.MODE_SEQUENTIAL if mode == "sequential" else N.MODE_HOGWILD)
+    st = eng.read_stats()
+    g0, g1 = eng.get_weights()
+    a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
+    ref = CO.train(tok, off, js, al.astype(np.float32), sd, CO.sample_int(counts, sample), True,
+                   CO.make_cum_table(counts), a0, a1, np.ones(V, np.float32), K)
+    assert (st["effective_words"], st["examples"]) == (ref["effective_words"], ref["examples"])
+    assert np.isfinite(g0).all() and np.isfinite(g1).all()
+    if mode == "sequential":
+        _close(g0, a0, atol=1e-6)
+        _close(g1, a1, atol=1e-6)
 
 
 def _eval_loss(syn0, syn1, tok, counts, K, n_eval=20000, seed=99):
