@@ -19,8 +19,9 @@ namespace g2v {
 // vs 2.77 sequential); atomics keep all of them (2.76).
 //
 // Pipelining: example e+1's record and rows are loaded BEFORE example e's
-// atomics are issued, so the loads never wait behind the atomics in the
-// wave's in-order vmcnt.  l1 and work are staged through LDS in element order
+// atomics are issued, so in the wave's in-order vmcnt they wait only behind
+// example e-1's atomics (the record load's wait drains those; a wave keeps at
+// most one example's atomics in flight).  l1 and work are staged through LDS in element order
 // so each atomic wave-instruction adds 64 contiguous floats (256 B); the
 // D % 64 tails of all K+2 rows are packed into shared instructions.
 template <int K, int NV>
