@@ -25,7 +25,7 @@ constexpr uint32_t kMaxJump = 1u << (2 * kJumpBits);
 constexpr int kBucketShift = 15;
 constexpr int kBuckets = 1 << (31 - kBucketShift);
 
-constexpr int kSampleThreads = 256;
+constexpr int kSampleThreads = 1024;
 constexpr int kSgnsThreads = 256;
 constexpr int kChunk = 32;  // consecutive examples a wave trains per grid-stride step
 
