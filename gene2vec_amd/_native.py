@@ -115,6 +115,15 @@ def lib():
         raise NativeLibraryError(
             f"{LIB_PATH} is missing: build it with `python -m gene2vec_amd.build` "
             "(the SGNS path has no CPU fallback)")
+    # torch bundles its own HIP runtime under the same soname
+    # (libamdhip64.so.7) as /opt/rocm's, which libg2v links.  Whichever loads
+    # first serves the whole process; torch fails on the other one ("no
+    # ROCm-capable device"), so torch's is loaded before libg2v and libg2v runs
+    # on it (measured on MI355X: libg2v first -> torch.cuda init fails).
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - torch is plumbing, not required
+        pass
     try:
         L = C.CDLL(LIB_PATH)
     except OSError as e:  # pragma: no cover - depends on the ROCm runtime

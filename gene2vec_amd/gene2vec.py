@@ -160,8 +160,13 @@ def main(argv=None):
               mode=args.mode)
     import gene2vec_amd.word2vec as W
     W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
+    prefetch = None
     for current_iter in range(1, args.iters + 1):
         name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
+        if corpus is not None and current_iter == 1 and args.iters > 1:
+            # the next iteration's reshuffle (:80) is drawn on a host thread
+            # while this one trains and exports (ShufflePrefetch)
+            prefetch = ingest.ShufflePrefetch(corpus.n_sent, rng, out=perm_buf)
         if current_iter == 1:
             print(f"gene2vec dimension {dimension} iteration {current_iter} start")
             if corpus is None:
@@ -183,8 +188,10 @@ def main(argv=None):
             print("shuffle start " + str(n_pairs))
             with ph("shuffle"):
                 if corpus is not None:
-                    perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng, out=perm_buf)
+                    perm_buf = prefetch.result()
                     corpus.permute_(perm_buf)
+                    if current_iter < args.iters:
+                        prefetch = ingest.ShufflePrefetch(corpus.n_sent, rng, out=perm_buf)
                 else:
                     rng.shuffle(gene_pairs)
             print(datetime.datetime.now())

@@ -109,3 +109,48 @@ def py_shuffle_perm(n, rng: random.Random, out=None):
     N.check(N.lib().g2v_py_shuffle_range(N.ptr(state), N.ptr(pos), N.ptr(perm), n))
     rng.setstate((version, tuple(int(x) for x in state) + (int(pos[0]),), gauss))
     return perm
+
+
+class ShufflePrefetch:
+    """The next ``py_shuffle_perm(n, rng)``, computed on a host thread while the
+    GPU trains the current iteration (src/gene2vec.py:80 reshuffles before every
+    iteration >= 2; the Fisher-Yates swaps depend only on n and the Mersenne
+    Twister state, not on the list's contents, so the permutation can be drawn
+    one iteration early).  ``result()`` joins, hands ``rng`` the state
+    ``rng.shuffle`` would have left and returns the permutation.  If anything
+    drew from ``rng`` after ``start`` the prefetched permutation is discarded and
+    recomputed from the live state, so the result is always what an in-place
+    ``rng.shuffle`` at ``result()`` time gives.  ctypes releases the GIL for the
+    native draw, so Python-side training and exports proceed meanwhile."""
+
+    def __init__(self, n, rng: random.Random, out=None):
+        import threading
+        self.n, self.rng = n, rng
+        self.snap = rng.getstate()
+        version, internal, gauss = self.snap
+        self.state = np.array(internal[:624], dtype=np.uint32)
+        self.pos = np.array([internal[624]], dtype=np.uint32)
+        if out is None or out.shape != (n,) or out.dtype != np.int64:
+            out = np.empty(n, dtype=np.int64)
+        self.perm = out
+        self.rc = None
+        self.th = threading.Thread(target=self._run, daemon=True)
+        self.th.start()
+
+    def _run(self):
+        self.rc = N.lib().g2v_py_shuffle_range(N.ptr(self.state), N.ptr(self.pos),
+                                               N.ptr(self.perm), self.n)
+        if self.rc != N.G2V_OK:  # g2v_last_error is thread-local: read it here
+            msg = N.lib().g2v_last_error()
+            self.err = N.G2VError(self.rc, msg.decode() if msg else "")
+
+    def result(self):
+        self.th.join()
+        if self.rc != N.G2V_OK:
+            raise self.err
+        if self.rng.getstate() != self.snap:  # rng was used meanwhile: redo from now
+            return py_shuffle_perm(self.n, self.rng, out=self.perm)
+        version, _, gauss = self.snap
+        self.rng.setstate((version, tuple(int(x) for x in self.state) + (int(self.pos[0]),),
+                           gauss))
+        return self.perm

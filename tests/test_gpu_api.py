@@ -93,9 +93,9 @@ def test_cli_native_ingest_equals_python_ingest(tmp_path):
     outs = {}
     for tag, extra in (("py", []), ("native", ["--native-ingest"])):
         out = tmp_path / tag
-        cli_main([str(data), str(out), "txt", "--iters", "2", "--dim", "64", "--mode",
+        cli_main([str(data), str(out), "txt", "--iters", "3", "--dim", "64", "--mode",
                   "sequential", "--hash", "crc32", "--shuffle-seed", "11", "--no-txt"] + extra)
-        outs[tag] = KeyedVectors.load_word2vec_format(str(out / "gene2vec_dim_64_iter_2_w2v.txt"))
+        outs[tag] = KeyedVectors.load_word2vec_format(str(out / "gene2vec_dim_64_iter_3_w2v.txt"))
     assert outs["py"].index2word == outs["native"].index2word
     np.testing.assert_array_equal(outs["py"].vectors, outs["native"].vectors)
 

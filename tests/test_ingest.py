@@ -4,7 +4,7 @@ import random
 import numpy as np
 import pytest
 
-from gene2vec_amd.ingest import py_shuffle_perm, read_corpus
+from gene2vec_amd.ingest import ShufflePrefetch, py_shuffle_perm, read_corpus
 
 
 def _py_read(paths):
@@ -77,6 +77,34 @@ def test_py_shuffle_perm_bit_compatible(n):
     assert perm.tolist() == data
     assert r1.getstate() == r2.getstate()
     assert r1.random() == r2.random()
+
+
+def test_shuffle_prefetch_chain_equals_in_place_shuffles():
+    """gene2vec.py's per-iteration reshuffle drawn one iteration early on a
+    host thread (ShufflePrefetch) == successive rng.shuffle calls (:52,:80)."""
+    n = 50021
+    r1, r2 = random.Random(99), random.Random(99)
+    data = list(range(n))
+    cur = np.arange(n)
+    buf = None
+    for _ in range(4):
+        r1.shuffle(data)
+        pf = ShufflePrefetch(n, r2, out=buf)
+        buf = pf.result()
+        cur = cur[buf]
+        assert cur.tolist() == data
+    assert r1.getstate() == r2.getstate()
+
+
+def test_shuffle_prefetch_discarded_when_rng_drawn_meanwhile():
+    r1, r2 = random.Random(5), random.Random(5)
+    pf = ShufflePrefetch(1000, r2)
+    r1.random()
+    r2.random()  # a draw between start and result: the prefetch is stale
+    data = list(range(1000))
+    r1.shuffle(data)
+    assert pf.result().tolist() == data
+    assert r1.getstate() == r2.getstate()
 
 
 def test_permuted_corpus_and_vocab(files):
