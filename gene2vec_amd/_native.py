@@ -99,8 +99,10 @@ SIGNATURES = {
     "g2v_corpus_export": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "g2v_corpus_free": (C.c_int, [_vp]),
     "g2v_csr_permute": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
+    "g2v_pairs_permute": (C.c_int, [_vp, _i64, _vp, _vp]),
     "g2v_py_shuffle": (C.c_int, [_vp, _vp, _vp, _i64]),
     "g2v_py_shuffle_range": (C.c_int, [_vp, _vp, _vp, _i64]),
+    "g2v_py_shuffle_skip": (C.c_int, [_vp, _vp, _i64]),
 }
 
 _lib = None

@@ -336,6 +336,40 @@ int g2v_corpus_export(const g2v_corpus* c, int32_t* tokens, int64_t* sent_off, i
   return G2V_OK;
 }
 
+int g2v_pairs_permute(const int32_t* tok, int64_t n_pairs, const int64_t* perm,
+                      int32_t* out_tok) {
+  if (n_pairs < 0 || (n_pairs > 0 && (!tok || !perm || !out_tok))) return G2V_EINVAL;
+  // one 8-byte random read per pair (the CSR form reads two offsets per pair
+  // in each of its two passes); output written sequentially
+  const int nt = (int)std::min<int64_t>(16, std::max<int64_t>(1, n_pairs >> 16));
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(tok);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(out_tok);
+  std::atomic<bool> bad{false};
+  std::vector<std::thread> th;
+  auto fn = [&](int t) {
+    const int64_t a = n_pairs * t / nt, b = n_pairs * (t + 1) / nt;
+    constexpr int64_t kAhead = 16;
+    for (int64_t i = a; i < b; ++i) {
+      if (i + kAhead < b) {
+        const int64_t q = perm[i + kAhead];
+        if (q >= 0 && q < n_pairs) __builtin_prefetch(src + q);
+      }
+      const int64_t p = perm[i];
+      if (p < 0 || p >= n_pairs) {
+        bad = true;
+        return;
+      }
+      uint64_t v;
+      memcpy(&v, src + p, 8);
+      dst[i] = v;
+    }
+  };
+  for (int t = 1; t < nt; ++t) th.emplace_back(fn, t);
+  fn(0);
+  for (auto& x : th) x.join();
+  return bad ? G2V_EINVAL : G2V_OK;
+}
+
 int g2v_csr_permute(const int32_t* tok, const int64_t* off, int64_t n_sent, const int64_t* perm,
                     int32_t* out_tok, int64_t* out_off) {
   if (n_sent < 0 || (n_sent > 0 && (!tok || !off || !perm || !out_tok || !out_off)))
@@ -419,9 +453,8 @@ struct PyMT {
     y ^= y >> 18;
     return y;
   }
-  uint64_t randbelow(uint64_t m) {
-    int k = 0;
-    for (uint64_t t = m; t; t >>= 1) ++k;
+  uint64_t randbelow(uint64_t m) {  // 2 <= m < 2^32
+    const int k = 64 - __builtin_clzll(m);
     for (;;) {
       const uint64_t r = next() >> (32 - k);
       if (r < m) return r;
@@ -436,9 +469,17 @@ int g2v_py_shuffle_range(uint32_t* state624, uint32_t* pos, int64_t* x, int64_t 
   return g2v_py_shuffle(state624, pos, x, n);
 }
 
+int g2v_py_shuffle_skip(uint32_t* state624, uint32_t* pos, int64_t n) {
+  if (!state624 || !pos) return G2V_EINVAL;
+  if (n >= ((int64_t)1 << 32)) return G2V_ERANGE;
+  PyMT r{state624, pos};
+  for (int64_t i = n - 1; i >= 1; --i) (void)r.randbelow((uint64_t)(i + 1));
+  return G2V_OK;
+}
+
 int g2v_py_shuffle(uint32_t* state624, uint32_t* pos, int64_t* x, int64_t n) {
   if (!state624 || !pos || (n > 0 && !x)) return G2V_EINVAL;
-  if (n > ((int64_t)1 << 32)) return G2V_ERANGE;
+  if (n >= ((int64_t)1 << 32)) return G2V_ERANGE;  // _randbelow(2^32) draws 2 words
   PyMT r{state624, pos};
   // same swaps in the same order; the j of a block are drawn first so the
   // random x[j] lines can be prefetched ahead of their swap

@@ -26,6 +26,8 @@ import random
 import time
 import zlib
 
+import numpy as np
+
 from . import generateMatrix as gM
 from . import ingest
 from .word2vec import Word2Vec
@@ -64,6 +66,30 @@ def _vocab_ids(model, corpus):
     voc = model.wv.vocab
     return np.array([voc[w].index if w in voc else -1 for w in corpus.words] or [0],
                     dtype=np.int32)
+
+
+def _adopt_vocab_ids(corpus, ids, tok):
+    """Renumber the corpus in the model's vocabulary order once (iteration 1),
+    when every corpus word is in the vocabulary (min_count = 1): the reloaded
+    model of iterations >= 2 keeps that vocabulary (src/gene2vec.py:86), so the
+    per-iteration 200 M-token remap becomes an O(V) identity check."""
+    import numpy as np
+    if len(ids) != len(corpus.words) or (ids < 0).any():
+        return
+    if len(np.unique(ids)) != len(ids):
+        return
+    words = [None] * len(ids)
+    for i, w in enumerate(corpus.words):
+        words[ids[i]] = w
+    counts = np.empty_like(corpus.counts)
+    counts[ids] = corpus.counts
+    corpus.tokens, corpus.words, corpus.counts = tok, words, counts
+
+
+def _sentences(corpus, pairs_only):
+    """train_ids' sentence layout: (None, 2) for an all-pairs corpus (same jobs
+    and sampled stream as its CSR form), else the CSR offsets"""
+    return (None, 2) if pairs_only else (corpus.sent_off, 0)
 
 
 class _Phases:
@@ -139,13 +165,20 @@ def main(argv=None):
         else:
             gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
             n_pairs = len(gene_pairs)
+        # every line a pair (the generator's output): fixed-length sentences,
+        # no 8-byte offsets per pair to upload; shuffles keep the lengths
+        pairs_only = corpus is not None and corpus.pairs_only
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
-    perm_buf = None
+    pipe = None
     with ph("shuffle"):
         if corpus is not None:
-            perm_buf = ingest.py_shuffle_perm(corpus.n_sent, rng)
-            corpus.permute_(perm_buf)
+            # this shuffle and the reshuffle before every later iteration (:80)
+            # are drawn ahead on host threads while the GPU trains
+            pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
+            perm = pipe.next()
+            corpus.permute_(perm)
+            pipe.release(perm)
         else:
             rng.shuffle(gene_pairs)
     print(datetime.datetime.now())
@@ -160,13 +193,8 @@ def main(argv=None):
               mode=args.mode)
     import gene2vec_amd.word2vec as W
     W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
-    prefetch = None
     for current_iter in range(1, args.iters + 1):
         name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
-        if corpus is not None and current_iter == 1 and args.iters > 1:
-            # the next iteration's reshuffle (:80) is drawn on a host thread
-            # while this one trains and exports (ShufflePrefetch)
-            prefetch = ingest.ShufflePrefetch(corpus.n_sent, rng, out=perm_buf)
         if current_iter == 1:
             print(f"gene2vec dimension {dimension} iteration {current_iter} start")
             if corpus is None:
@@ -180,18 +208,18 @@ def main(argv=None):
                     model.corpus_total_words = int(corpus.sent_off[-1])
                     ids = _vocab_ids(model, corpus)
                     tok = ids[corpus.tokens]
+                    _adopt_vocab_ids(corpus, ids, tok)
                 with ph("train"):
-                    model.train_ids(tok, corpus.sent_off,
+                    model.train_ids(tok, *_sentences(corpus, pairs_only),
                                     total_examples=model.corpus_count, epochs=model.iter)
         else:
             print(datetime.datetime.now())
             print("shuffle start " + str(n_pairs))
             with ph("shuffle"):
                 if corpus is not None:
-                    perm_buf = prefetch.result()
-                    corpus.permute_(perm_buf)
-                    if current_iter < args.iters:
-                        prefetch = ingest.ShufflePrefetch(corpus.n_sent, rng, out=perm_buf)
+                    perm = pipe.next()
+                    corpus.permute_(perm)
+                    pipe.release(perm)
                 else:
                     rng.shuffle(gene_pairs)
             print(datetime.datetime.now())
@@ -205,9 +233,13 @@ def main(argv=None):
                     model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
             else:
                 with ph("vocab"):
-                    tok = _vocab_ids(model, corpus)[corpus.tokens]
+                    ids = _vocab_ids(model, corpus)
+                    if np.array_equal(ids, np.arange(len(ids), dtype=np.int32)):
+                        tok = corpus.tokens  # adopted at iteration 1: ids are the model's
+                    else:
+                        tok = ids[corpus.tokens]
                 with ph("train"):
-                    model.train_ids(tok, corpus.sent_off,
+                    model.train_ids(tok, *_sentences(corpus, pairs_only),
                                     total_examples=model.corpus_count, epochs=model.iter)
         with ph("save"):
             model._sync_host()

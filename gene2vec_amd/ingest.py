@@ -30,6 +30,15 @@ class Corpus:
     def n_sent(self):
         return len(self.sent_off) - 1
 
+    @property
+    def pairs_only(self):
+        """every sentence is exactly 2 tokens (the pair generator's output);
+        checked once, permutations keep it"""
+        if getattr(self, "_pairs_only", None) is None:
+            self._pairs_only = bool(np.array_equal(
+                self.sent_off, np.arange(0, 2 * self.n_sent + 1, 2, dtype=np.int64)))
+        return self._pairs_only
+
     def sentences(self):
         """materialise list[list[str]] (small corpora / tests)"""
         w = self.words
@@ -51,6 +60,16 @@ class Corpus:
         buffers kept from the previous call (no fresh 2 x 160 MB allocation
         and page faults per iteration at 20 M pairs), then the buffers swap."""
         perm = np.ascontiguousarray(perm, dtype=np.int64)
+        if self.pairs_only:
+            if len(perm) != self.n_sent:
+                raise ValueError("permutation length != number of sentences")
+            spare = getattr(self, "_spare_tok", None)
+            if spare is None or spare.shape != self.tokens.shape:
+                spare = np.empty_like(self.tokens)
+            N.check(N.lib().g2v_pairs_permute(N.ptr(self.tokens), self.n_sent, N.ptr(perm),
+                                              N.ptr(spare)))
+            self._spare_tok, self.tokens = self.tokens, spare
+            return self
         spare = getattr(self, "_spare", None)
         if spare is None or spare[0].shape != self.tokens.shape:
             spare = (np.empty_like(self.tokens), np.empty_like(self.sent_off))
@@ -111,46 +130,95 @@ def py_shuffle_perm(n, rng: random.Random, out=None):
     return perm
 
 
-class ShufflePrefetch:
-    """The next ``py_shuffle_perm(n, rng)``, computed on a host thread while the
-    GPU trains the current iteration (src/gene2vec.py:80 reshuffles before every
-    iteration >= 2; the Fisher-Yates swaps depend only on n and the Mersenne
-    Twister state, not on the list's contents, so the permutation can be drawn
-    one iteration early).  ``result()`` joins, hands ``rng`` the state
-    ``rng.shuffle`` would have left and returns the permutation.  If anything
-    drew from ``rng`` after ``start`` the prefetched permutation is discarded and
-    recomputed from the live state, so the result is always what an in-place
-    ``rng.shuffle`` at ``result()`` time gives.  ctypes releases the GIL for the
-    native draw, so Python-side training and exports proceed meanwhile."""
+class ShufflePipeline:
+    """The ``count`` successive ``py_shuffle_perm(n, rng)`` of the CLI
+    (src/gene2vec.py:52 once, :80 before every iteration >= 2), drawn ahead
+    on host threads while the GPU trains.  Fisher-Yates swaps depend only on n
+    and the Mersenne Twister state, never on the list, so shuffle k+1's state
+    is known as soon as shuffle k's draws are replayed (``g2v_py_shuffle_skip``,
+    no swaps): a driver thread replays the draws and starts each shuffle's
+    memory-bound swaps on a thread of its own, at most ``depth`` permutations
+    alive at once (``release`` hands one back).  ``next()`` returns the next
+    permutation and leaves ``rng`` in the state ``rng.shuffle`` would; if
+    anything else drew from ``rng`` meanwhile the pipeline is dropped and the
+    permutation recomputed from the live state, so the results always equal
+    in-place ``rng.shuffle`` calls.  ctypes releases the GIL for the native
+    calls."""
 
-    def __init__(self, n, rng: random.Random, out=None):
+    def __init__(self, n, rng: random.Random, count, depth=2):
+        import queue
         import threading
-        self.n, self.rng = n, rng
-        self.snap = rng.getstate()
-        version, internal, gauss = self.snap
-        self.state = np.array(internal[:624], dtype=np.uint32)
-        self.pos = np.array([internal[624]], dtype=np.uint32)
-        if out is None or out.shape != (n,) or out.dtype != np.int64:
-            out = np.empty(n, dtype=np.int64)
-        self.perm = out
-        self.rc = None
-        self.th = threading.Thread(target=self._run, daemon=True)
-        self.th.start()
+        self.n, self.rng, self.count = n, rng, count
+        self.expect = rng.getstate()
+        version, internal, gauss = self.expect
+        self.meta = (version, gauss)
+        self.cond = threading.Condition()
+        self.perm, self.after, self.err = {}, {}, None
+        self.k = 0
+        self.dead = False
+        self.free = queue.Queue()
+        for _ in range(depth):
+            self.free.put(None)
+        st = np.array(internal[:624], dtype=np.uint32)
+        pos = np.array([internal[624]], dtype=np.uint32)
+        self.driver = threading.Thread(target=self._drive, args=(st, pos), daemon=True)
+        self.driver.start()
 
-    def _run(self):
-        self.rc = N.lib().g2v_py_shuffle_range(N.ptr(self.state), N.ptr(self.pos),
-                                               N.ptr(self.perm), self.n)
-        if self.rc != N.G2V_OK:  # g2v_last_error is thread-local: read it here
-            msg = N.lib().g2v_last_error()
-            self.err = N.G2VError(self.rc, msg.decode() if msg else "")
+    def _fail(self, rc):
+        msg = N.lib().g2v_last_error()  # thread-local: read it on this thread
+        with self.cond:
+            self.err = N.G2VError(rc, msg.decode() if msg else "")
+            self.cond.notify_all()
 
-    def result(self):
-        self.th.join()
-        if self.rc != N.G2V_OK:
-            raise self.err
-        if self.rng.getstate() != self.snap:  # rng was used meanwhile: redo from now
-            return py_shuffle_perm(self.n, self.rng, out=self.perm)
-        version, _, gauss = self.snap
-        self.rng.setstate((version, tuple(int(x) for x in self.state) + (int(self.pos[0]),),
-                           gauss))
-        return self.perm
+    def _drive(self, st, pos):
+        import threading
+        L = N.lib()
+        for k in range(self.count):
+            buf = self.free.get()
+            if self.dead:
+                return
+            threading.Thread(target=self._swaps, args=(k, st.copy(), pos.copy(), buf),
+                             daemon=True).start()
+            rc = L.g2v_py_shuffle_skip(N.ptr(st), N.ptr(pos), self.n)
+            if rc != N.G2V_OK:
+                return self._fail(rc)
+            with self.cond:
+                self.after[k] = (st.copy(), int(pos[0]))
+                self.cond.notify_all()
+
+    def _swaps(self, k, st, pos, buf):
+        perm = buf if buf is not None else np.empty(self.n, dtype=np.int64)
+        rc = N.lib().g2v_py_shuffle_range(N.ptr(st), N.ptr(pos), N.ptr(perm), self.n)
+        if rc != N.G2V_OK:
+            return self._fail(rc)
+        with self.cond:
+            self.perm[k] = perm
+            self.cond.notify_all()
+
+    def next(self):
+        if self.k >= self.count:
+            raise IndexError("ShufflePipeline: all permutations consumed")
+        k = self.k
+        self.k += 1
+        if self.dead or self.rng.getstate() != self.expect:
+            self.close()
+            return py_shuffle_perm(self.n, self.rng)
+        with self.cond:
+            self.cond.wait_for(lambda: self.err is not None or (k in self.perm and k in self.after))
+            if self.err is not None:
+                raise self.err
+            perm = self.perm.pop(k)
+            st, pos = self.after.pop(k)
+        version, gauss = self.meta
+        self.rng.setstate((version, tuple(int(x) for x in st) + (pos,), gauss))
+        self.expect = self.rng.getstate()
+        return perm
+
+    def release(self, perm):
+        """perm (from next()) is no longer needed: its buffer serves a later shuffle"""
+        if not self.dead:
+            self.free.put(perm)
+
+    def close(self):
+        self.dead = True
+        self.free.put(None)  # wakes a driver blocked on a buffer

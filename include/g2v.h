@@ -250,11 +250,18 @@ int g2v_corpus_free(g2v_corpus *c);
 /* out sentence i = in sentence perm[i] (CSR gather) */
 int g2v_csr_permute(const int32_t *tok, const int64_t *off, int64_t n_sent, const int64_t *perm,
                     int32_t *out_tok, int64_t *out_off);
+/* all-pairs corpus (every sentence 2 tokens, offsets 2*i): out pair i = in
+ * pair perm[i]; the offsets are unchanged by any permutation */
+int g2v_pairs_permute(const int32_t *tok, int64_t n_pairs, const int64_t *perm, int32_t *out_tok);
 /* CPython random.Random.shuffle(x) bit for bit; state624/pos = getstate()[1][:625],
  * updated in place (setstate afterwards keeps Python's generator in step). */
 int g2v_py_shuffle(uint32_t *state624, uint32_t *pos, int64_t *x, int64_t n);
 /* x = range(n), then g2v_py_shuffle (the permutation gene2vec.py:52,80 applies). */
 int g2v_py_shuffle_range(uint32_t *state624, uint32_t *pos, int64_t *x, int64_t n);
+/* the generator state g2v_py_shuffle(n) leaves, without the swaps (the draws
+ * do not depend on the list): lets the CLI draw later iterations' reshuffles
+ * (gene2vec.py:80) concurrently. */
+int g2v_py_shuffle_skip(uint32_t *state624, uint32_t *pos, int64_t n);
 
 #ifdef __cplusplus
 }

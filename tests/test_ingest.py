@@ -4,7 +4,8 @@ import random
 import numpy as np
 import pytest
 
-from gene2vec_amd.ingest import ShufflePrefetch, py_shuffle_perm, read_corpus
+from gene2vec_amd import _native as N
+from gene2vec_amd.ingest import ShufflePipeline, py_shuffle_perm, read_corpus
 
 
 def _py_read(paths):
@@ -79,31 +80,49 @@ def test_py_shuffle_perm_bit_compatible(n):
     assert r1.random() == r2.random()
 
 
-def test_shuffle_prefetch_chain_equals_in_place_shuffles():
-    """gene2vec.py's per-iteration reshuffle drawn one iteration early on a
-    host thread (ShufflePrefetch) == successive rng.shuffle calls (:52,:80)."""
+@pytest.mark.parametrize("n", [0, 1, 2, 1000, 123457])
+def test_py_shuffle_skip_leaves_shuffle_state(n):
+    """g2v_py_shuffle_skip replays shuffle(n)'s draws without the swaps"""
+    r1 = random.Random(2024)
+    r1.shuffle(list(range(n)))
+    st = np.array(random.Random(2024).getstate()[1][:624], dtype=np.uint32)
+    pos = np.array([random.Random(2024).getstate()[1][624]], dtype=np.uint32)
+    N.check(N.lib().g2v_py_shuffle_skip(N.ptr(st), N.ptr(pos), n))
+    assert tuple(int(x) for x in st) + (int(pos[0]),) == r1.getstate()[1]
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_shuffle_pipeline_equals_in_place_shuffles(depth):
+    """gene2vec.py's shuffle (:52) and per-iteration reshuffles (:80) drawn
+    ahead on host threads (ShufflePipeline) == successive rng.shuffle calls."""
     n = 50021
     r1, r2 = random.Random(99), random.Random(99)
     data = list(range(n))
     cur = np.arange(n)
-    buf = None
-    for _ in range(4):
+    pipe = ShufflePipeline(n, r2, 5, depth=depth)
+    for _ in range(5):
         r1.shuffle(data)
-        pf = ShufflePrefetch(n, r2, out=buf)
-        buf = pf.result()
-        cur = cur[buf]
+        perm = pipe.next()
+        cur = cur[perm]
+        pipe.release(perm)
         assert cur.tolist() == data
-    assert r1.getstate() == r2.getstate()
+        assert r1.getstate() == r2.getstate()
+    with pytest.raises(IndexError):
+        pipe.next()
 
 
-def test_shuffle_prefetch_discarded_when_rng_drawn_meanwhile():
+def test_shuffle_pipeline_dropped_when_rng_drawn_meanwhile():
     r1, r2 = random.Random(5), random.Random(5)
-    pf = ShufflePrefetch(1000, r2)
-    r1.random()
-    r2.random()  # a draw between start and result: the prefetch is stale
+    pipe = ShufflePipeline(1000, r2, 3)
     data = list(range(1000))
     r1.shuffle(data)
-    assert pf.result().tolist() == data
+    assert pipe.next().tolist() == data
+    r1.random()
+    r2.random()  # a draw between two shuffles: the pipeline is stale
+    for _ in range(2):
+        data = list(range(1000))
+        r1.shuffle(data)
+        assert pipe.next().tolist() == data
     assert r1.getstate() == r2.getstate()
 
 
@@ -154,3 +173,28 @@ def test_native_reader_long_words_table_growth_and_chunks(tmp_path):
         idx = {w: i for i, w in enumerate(fo)}
         flat = np.array([idx[w] for s in ref for w in s], np.int32)
         assert np.array_equal(c.tokens, flat)
+
+
+def test_pairs_permute_equals_csr_permute():
+    """all-pairs corpora take the 8-byte pair gather (g2v_pairs_permute);
+    the result equals the CSR gather, offsets untouched"""
+    from gene2vec_amd.ingest import Corpus
+    rs = np.random.RandomState(1)
+    n = 200003
+    tok = rs.randint(0, 5000, 2 * n).astype(np.int32)
+    off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
+    perm = py_shuffle_perm(n, random.Random(3))
+    a = Corpus(tok.copy(), off.copy(), [], None)
+    assert a.pairs_only
+    a.permute_(perm)
+    a.permute_(perm)  # second call reuses the spare buffer
+    ref = tok.reshape(n, 2)[perm][perm].ravel()
+    np.testing.assert_array_equal(a.tokens, ref)
+    np.testing.assert_array_equal(a.sent_off, off)
+    mixed = Corpus(np.arange(5, dtype=np.int32), np.array([0, 2, 5], dtype=np.int64), [], None)
+    assert not mixed.pairs_only
+    mixed.permute_(np.array([1, 0]))
+    np.testing.assert_array_equal(mixed.tokens, [2, 3, 4, 0, 1])
+    np.testing.assert_array_equal(mixed.sent_off, [0, 3, 5])
+    with pytest.raises(N.G2VError):
+        Corpus(tok.copy(), off.copy(), [], None).permute_(np.full(n, n, dtype=np.int64))

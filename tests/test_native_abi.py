@@ -92,3 +92,12 @@ def test_count_ids():
     ids = np.array([3, 1, 3, 0, 3, 1], np.int32)
     c, f = E.count_ids(ids, 5)
     assert c.tolist() == [1, 2, 0, 3, 0] and f.tolist() == [3, 1, -1, 0, -1]
+
+
+@pytest.mark.parametrize("n", [0, 1, 4999, 5000, 5001, 123457])
+def test_plan_jobs_fixed_pairs_equal_csr_pairs(n):
+    """The CLI trains an all-pairs corpus as fixed-length sentences (sent_len=2):
+    its gensim jobs must equal the CSR form's."""
+    csr = E.plan_jobs(sent_off=np.arange(0, 2 * n + 1, 2, dtype=np.int64))
+    fixed = E.plan_jobs(n_sent=n, sent_len=2)
+    np.testing.assert_array_equal(csr, fixed)
