@@ -122,6 +122,9 @@ def lib():
     # first serves the whole process; torch fails on the other one ("no
     # ROCm-capable device"), so torch's is loaded before libg2v and libg2v runs
     # on it (measured on MI355X: libg2v first -> torch.cuda init fails).
+    # `import torch` itself, not just a dlopen of torch's libamdhip64: with the
+    # dlopen alone the CLI's 10 training iterations took 19.4 s instead of
+    # 7.3 s on MI355X (profiles/r01_e2e_cli_100m.json), for the 1.5 s import.
     try:
         import torch  # noqa: F401
     except ImportError:  # pragma: no cover - torch is plumbing, not required
