@@ -82,13 +82,19 @@ def test_cli_end_to_end_matches_oracle(tmp_path, test_pairs):
                                rtol=1e-5, atol=1e-7)
 
 
-def test_cli_native_ingest_equals_python_ingest(tmp_path):
+@pytest.mark.parametrize("ragged", [False, True])
+def test_cli_native_ingest_equals_python_ingest(tmp_path, ragged):
+    """all-pairs files take the pair-gather / fixed-length path, ragged ones
+    (a 4-token study-boundary line, an empty line) the CSR path"""
     data = tmp_path / "data"
     data.mkdir()
     rng = np.random.RandomState(3)
     genes = [f"G{i}" for i in range(400)]
     for k in range(3):
         lines = [f"{genes[a]} {genes[b]}" for a, b in rng.randint(0, 400, (3000, 2)) if a != b]
+        if ragged and k == 1:
+            lines[10] = "G1 G2 G3 G4"
+            lines[20] = ""
         (data / f"s{k}.txt").write_text("\n".join(lines) + ("\n" if k else ""))
     outs = {}
     for tag, extra in (("py", []), ("native", ["--native-ingest"])):
