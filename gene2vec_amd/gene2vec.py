@@ -92,6 +92,41 @@ def _sentences(corpus, pairs_only):
     return (None, 2) if pairs_only else (corpus.sent_off, 0)
 
 
+class _Exporter:
+    """per-iteration text exports on one background thread (src/gene2vec.py:89
+    generateMatrix + the _w2v.txt the target function reads); a failure is
+    raised at the next submit or at close()"""
+
+    def __init__(self, txt, w2v, w2v_binary):
+        from concurrent.futures import ThreadPoolExecutor
+        self.txt, self.w2v, self.w2v_binary = txt, w2v, w2v_binary
+        self.pool = ThreadPoolExecutor(max_workers=1)
+        self.pending = None
+
+    def _run(self, name, wv, ph):
+        with ph("txt"):
+            if self.txt:
+                gM.outputTxt(name)
+        with ph("w2v"):
+            if self.w2v:
+                wv.save_word2vec_format(name + "_w2v.txt", binary=False)
+                if self.w2v_binary:
+                    wv.save_word2vec_format(name + "_w2v.bin", binary=True)
+
+    def submit(self, name, wv, ph):
+        if self.pending is not None:
+            self.pending.result()
+        self.pending = self.pool.submit(self._run, name, wv, ph)
+
+    def close(self):
+        try:
+            if self.pending is not None:
+                self.pending.result()
+        finally:
+            self.pending = None
+            self.pool.shutdown(wait=True)
+
+
 class _Phases:
     """wall seconds per CLI phase, summed over iterations (``--timing``)"""
 
@@ -170,6 +205,7 @@ def main(argv=None):
         pairs_only = corpus is not None and corpus.pairs_only
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
+    exporter = _Exporter(not args.no_txt, not args.no_w2v, args.w2v_binary)
     pipe = None
     with ph("shuffle"):
         if corpus is not None:
@@ -245,20 +281,19 @@ def main(argv=None):
             model._sync_host()
             if rank == 0:  # data parallel: the merged replicas are identical
                 model.save(name)
-        with ph("txt"):
-            if not args.no_txt and rank == 0:
-                gM.outputTxt(name)
-        with ph("w2v"):
-            if not args.no_w2v and rank == 0:
-                model.wv.save_word2vec_format(name + "_w2v.txt", binary=False)
-                if args.w2v_binary:
-                    model.wv.save_word2vec_format(name + "_w2v.bin", binary=True)
+        if rank == 0:
+            # the text exports (generateMatrix.py, save_word2vec_format) read
+            # this iteration's checkpoint / tables only: they run on a host
+            # thread while the next iteration trains (one at a time, in order)
+            exporter.submit(name, model.wv, ph)
         if world > 1:
             import torch.distributed as dist
             dist.barrier()  # the next iteration loads rank 0's checkpoint
         print(f"gene2vec dimension {dimension} iteration {current_iter} done")
         outputs.append(name)
         del model
+    with ph("export_wait"):
+        exporter.close()
     if args.timing and rank == 0:
         with open(args.timing, "w") as f:
             json.dump({k: round(v, 4) for k, v in ph.t.items()}, f)
