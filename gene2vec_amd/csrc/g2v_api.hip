@@ -683,6 +683,22 @@ int g2v_plan_jobs(const int64_t* sent_off, int64_t n_sent, int64_t sent_len, int
   REQUIRE(n_sent >= 0 && batch_words > 0, G2V_EINVAL, "bad sizes");
   REQUIRE(sent_len > 0 || sent_off, G2V_EINVAL, "need sent_off or sent_len > 0");
   // [ext] _job_producer: `if batch_size + len <= batch_words: append else: push`
+  if (sent_len > 0) {
+    // fixed-length sentences: the loop below packs exactly
+    // floor(batch_words / sent_len) sentences per job, so the starts are a
+    // closed form (no O(n_sent) pass per train() call: 100 M pairs cost 73 ms)
+    REQUIRE(n_sent == 0 || sent_len <= batch_words, G2V_ERANGE,
+            "sentence 0 has %lld tokens > batch_words %lld (unsupported)", (long long)sent_len,
+            (long long)batch_words);
+    const int64_t per = n_sent ? batch_words / sent_len : 1;
+    const int64_t nj = (n_sent + per - 1) / per;
+    if (job_sent)
+      for (int64_t j = 0; j <= nj && j < cap; ++j) job_sent[j] = j < nj ? j * per : n_sent;
+    *n_jobs_out = nj;
+    if (job_sent && cap < nj + 1)
+      return fail(G2V_ERANGE, "job_sent capacity %lld < %lld", (long long)cap, (long long)(nj + 1));
+    return G2V_OK;
+  }
   int64_t nj = 0, size = 0, start = 0;
   auto emit = [&](int64_t s) {
     if (job_sent && nj < cap) job_sent[nj] = s;

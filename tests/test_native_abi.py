@@ -94,10 +94,17 @@ def test_count_ids():
     assert c.tolist() == [1, 2, 0, 3, 0] and f.tolist() == [3, 1, -1, 0, -1]
 
 
+@pytest.mark.parametrize("sent_len", [1, 2, 3, 7, 10000])
 @pytest.mark.parametrize("n", [0, 1, 4999, 5000, 5001, 123457])
-def test_plan_jobs_fixed_pairs_equal_csr_pairs(n):
-    """The CLI trains an all-pairs corpus as fixed-length sentences (sent_len=2):
-    its gensim jobs must equal the CSR form's."""
-    csr = E.plan_jobs(sent_off=np.arange(0, 2 * n + 1, 2, dtype=np.int64))
-    fixed = E.plan_jobs(n_sent=n, sent_len=2)
+def test_plan_jobs_fixed_length_equal_csr(n, sent_len):
+    """Fixed-length sentences (the CLI trains an all-pairs corpus with
+    sent_len=2) take a closed form; its gensim jobs must equal the CSR loop's."""
+    csr = E.plan_jobs(sent_off=np.arange(0, sent_len * n + 1, sent_len, dtype=np.int64))
+    fixed = E.plan_jobs(n_sent=n, sent_len=sent_len)
     np.testing.assert_array_equal(csr, fixed)
+
+
+def test_plan_jobs_fixed_length_over_batch_words():
+    with pytest.raises(N.G2VError):
+        E.plan_jobs(n_sent=3, sent_len=N.BATCH_WORDS + 1)
+    np.testing.assert_array_equal(E.plan_jobs(n_sent=0, sent_len=N.BATCH_WORDS + 1), [0])
