@@ -29,7 +29,7 @@ for var in sys.argv[3].split(","):
     grid, late, ppm = map(int, var.split(":")); mode = N.MODE_HOGWILD
     eng = E.SGNSEngine(V, D, K); eng.set_vocab(counts, sample)
     eng.set_option(N.OPT_GRID, grid); eng.set_option(N.OPT_GRID_LATE, late)
-    eng.set_option(N.OPT_GRID_LATE_ALPHA_PPM, ppm)
+    eng.set_option(N.OPT_GRID_LATE_ALPHA_PPM, ppm); eng.set_option(N.OPT_SEG_JOBS, 100)
     eng.set_weights(syn0, np.zeros((V, D), np.float32)); eng.set_corpus(tok, sent_len=2)
     rs = np.random.RandomState(1)
     for it in range(ITERS):
