@@ -32,8 +32,6 @@ OPT_TABLE_MEM = 5
 OPT_DEBUG_WRITE = 6
 OPT_STRIPE_ROWS = 7
 OPT_STRIPE_COPIES = 8
-OPT_GRID_LATE = 9
-OPT_GRID_LATE_ALPHA_PPM = 10
 BATCH_WORDS = 10000
 MAX_DIM = 512
 TXT_MATRIX = 0

@@ -96,8 +96,6 @@ struct g2v_ctx {
   int nv = 1, nvec = 0, rec_stride = 0;
   int64_t ld = 0;
   int cus = 0, sgns_grid = 0;
-  int grid_late = 0;          // G2V_OPT_GRID_LATE (0 = off)
-  double grid_late_alpha = 0;  // segments whose first-job alpha <= this use grid_late
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
@@ -376,14 +374,6 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value >= 0 && value <= 4, G2V_EINVAL, "debug write mode out of [0, 4]");
       c->debug_write = (int)value;
       return G2V_OK;
-    case G2V_OPT_GRID_LATE:
-      REQUIRE(value >= 0, G2V_EINVAL, "late grid must be >= 0");
-      c->grid_late = (int)value;
-      return G2V_OK;
-    case G2V_OPT_GRID_LATE_ALPHA_PPM:
-      REQUIRE(value >= 0, G2V_EINVAL, "late-grid alpha must be >= 0");
-      c->grid_late_alpha = (double)value * 1e-6;
-      return G2V_OK;
     case G2V_OPT_GRID:
       REQUIRE(value >= 0, G2V_EINVAL, "grid must be >= 0");
       c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv);
@@ -632,7 +622,7 @@ static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing) {
 }
 
 static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool timing,
-                    const float* rd0, const float* rd1, int grid) {
+                    const float* rd0, const float* rd1) {
   SgnsArgs s{};
   s.rec = c->d_rec;
   s.rec_stride = c->rec_stride;
@@ -674,7 +664,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
     HIPCHK(hipEventRecord(e0, c->stream));
   }
-  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, grid, c->stream));
+  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
   HIPCHK(launch_fold_stripes(c->syn0, c->syn1, c->stripe, s.stripe_rows, s.stripe_copies, c->ld,
                              c->nvec, c->stream));
   if (timing) {
@@ -752,12 +742,7 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
   for (int64_t j0 = 0; j0 < n_jobs; j0 += c->seg_jobs) {
     const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
     if ((rc = sample_segment(c, j0, nj, timing))) return rc;
-    // Hogwild staleness scales with alpha x waves in flight: late in the
-    // alpha schedule a larger grid may stay stable (G2V_OPT_GRID_LATE)
-    const bool late = c->grid_late > 0 && (double)job_alpha[j0] <= c->grid_late_alpha;
-    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, c->syn0, c->syn1,
-                       late ? c->grid_late : c->sgns_grid)))
-      return rc;
+    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, c->syn0, c->syn1))) return rc;
   }
   c->jobs += n_jobs;
   return G2V_OK;
@@ -841,8 +826,7 @@ int g2v_sgns_step_explicit(g2v_ctx* c, const int32_t* center, const int32_t* inp
     rd0 = c->snap0;
     rd1 = c->snap1;
   }
-  if ((rc = run_sgns(c, c->d_job_exoff, mode, flags & G2V_FLAG_TIMING, rd0, rd1, c->sgns_grid)))
-    return rc;
+  if ((rc = run_sgns(c, c->d_job_exoff, mode, flags & G2V_FLAG_TIMING, rd0, rd1))) return rc;
   // host arrays were copied asynchronously from pageable memory: finish before returning
   HIPCHK(hipStreamSynchronize(c->stream));
   return G2V_OK;

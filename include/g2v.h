@@ -112,10 +112,6 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_DEBUG_WRITE 6
 #define G2V_OPT_STRIPE_ROWS 7
 #define G2V_OPT_STRIPE_COPIES 8
-/*   G2V_OPT_GRID_LATE     SGNS workgroups for segments whose first job's alpha is
- *                         <= G2V_OPT_GRID_LATE_ALPHA_PPM * 1e-6 (0 = off) [0] */
-#define G2V_OPT_GRID_LATE 9
-#define G2V_OPT_GRID_LATE_ALPHA_PPM 10
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);
