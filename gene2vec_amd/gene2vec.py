@@ -220,78 +220,83 @@ def main(argv=None):
     print(datetime.datetime.now())
     print("shuffle done " + str(n_pairs))
 
-    dimension = args.dim
-    hashfxn = _hashfxn(args.hash)
-    os.makedirs(export_dir, exist_ok=True)
-    outputs = []
-    kw = dict(size=dimension, window=args.window, min_count=1, workers=args.workers, iter=1, sg=1,
-              negative=args.negative, sample=args.sample, hashfxn=hashfxn, device=args.device,
-              mode=args.mode)
-    import gene2vec_amd.word2vec as W
-    W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
-    for current_iter in range(1, args.iters + 1):
-        name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
-        if current_iter == 1:
-            print(f"gene2vec dimension {dimension} iteration {current_iter} start")
-            if corpus is None:
-                with ph("train"):
-                    model = Word2Vec(gene_pairs, **kw)
-            else:
-                with ph("vocab"):
-                    model = Word2Vec(**kw)
-                    model._build_from_counts(corpus.vocab_raw_counts())
-                    model.corpus_count = corpus.n_sent
-                    model.corpus_total_words = int(corpus.sent_off[-1])
-                    ids = _vocab_ids(model, corpus)
-                    tok = ids[corpus.tokens]
-                    _adopt_vocab_ids(corpus, ids, tok)
-                with ph("train"):
-                    model.train_ids(tok, *_sentences(corpus, pairs_only),
-                                    total_examples=model.corpus_count, epochs=model.iter)
-        else:
-            print(datetime.datetime.now())
-            print("shuffle start " + str(n_pairs))
-            with ph("shuffle"):
-                if corpus is not None:
-                    perm = pipe.next()
-                    corpus.permute_(perm)
-                    pipe.release(perm)
+    try:
+        dimension = args.dim
+        hashfxn = _hashfxn(args.hash)
+        os.makedirs(export_dir, exist_ok=True)
+        outputs = []
+        kw = dict(size=dimension, window=args.window, min_count=1, workers=args.workers, iter=1,
+                  sg=1, negative=args.negative, sample=args.sample, hashfxn=hashfxn,
+                  device=args.device, mode=args.mode)
+        import gene2vec_amd.word2vec as W
+        W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
+        for current_iter in range(1, args.iters + 1):
+            name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
+            if current_iter == 1:
+                print(f"gene2vec dimension {dimension} iteration {current_iter} start")
+                if corpus is None:
+                    with ph("train"):
+                        model = Word2Vec(gene_pairs, **kw)
                 else:
-                    rng.shuffle(gene_pairs)
-            print(datetime.datetime.now())
-            print("shuffle done " + str(n_pairs))
-            print(f"gene2vec dimension {dimension} iteration {current_iter} start")
-            prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
-            with ph("load"):
-                model = Word2Vec.load(prev, device=args.device)
-            if corpus is None:
-                with ph("train"):
-                    model.train(gene_pairs, total_examples=model.corpus_count, epochs=model.iter)
-            else:
-                with ph("vocab"):
-                    ids = _vocab_ids(model, corpus)
-                    if np.array_equal(ids, np.arange(len(ids), dtype=np.int32)):
-                        tok = corpus.tokens  # adopted at iteration 1: ids are the model's
-                    else:
+                    with ph("vocab"):
+                        model = Word2Vec(**kw)
+                        model._build_from_counts(corpus.vocab_raw_counts())
+                        model.corpus_count = corpus.n_sent
+                        model.corpus_total_words = int(corpus.sent_off[-1])
+                        ids = _vocab_ids(model, corpus)
                         tok = ids[corpus.tokens]
-                with ph("train"):
-                    model.train_ids(tok, *_sentences(corpus, pairs_only),
-                                    total_examples=model.corpus_count, epochs=model.iter)
-        with ph("save"):
-            model._sync_host()
-            if rank == 0:  # data parallel: the merged replicas are identical
-                model.save(name)
-        if rank == 0:
-            # the text exports (generateMatrix.py, save_word2vec_format) read
-            # this iteration's checkpoint / tables only: they run on a host
-            # thread while the next iteration trains (one at a time, in order)
-            exporter.submit(name, model.wv, ph)
-        if world > 1:
-            import torch.distributed as dist
-            dist.barrier()  # the next iteration loads rank 0's checkpoint
-        print(f"gene2vec dimension {dimension} iteration {current_iter} done")
-        outputs.append(name)
-        del model
+                        _adopt_vocab_ids(corpus, ids, tok)
+                    with ph("train"):
+                        model.train_ids(tok, *_sentences(corpus, pairs_only),
+                                        total_examples=model.corpus_count, epochs=model.iter)
+            else:
+                print(datetime.datetime.now())
+                print("shuffle start " + str(n_pairs))
+                with ph("shuffle"):
+                    if corpus is not None:
+                        perm = pipe.next()
+                        corpus.permute_(perm)
+                        pipe.release(perm)
+                    else:
+                        rng.shuffle(gene_pairs)
+                print(datetime.datetime.now())
+                print("shuffle done " + str(n_pairs))
+                print(f"gene2vec dimension {dimension} iteration {current_iter} start")
+                prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
+                with ph("load"):
+                    model = Word2Vec.load(prev, device=args.device)
+                if corpus is None:
+                    with ph("train"):
+                        model.train(gene_pairs, total_examples=model.corpus_count,
+                                    epochs=model.iter)
+                else:
+                    with ph("vocab"):
+                        ids = _vocab_ids(model, corpus)
+                        if np.array_equal(ids, np.arange(len(ids), dtype=np.int32)):
+                            tok = corpus.tokens  # adopted at iteration 1: ids are the model's
+                        else:
+                            tok = ids[corpus.tokens]
+                    with ph("train"):
+                        model.train_ids(tok, *_sentences(corpus, pairs_only),
+                                        total_examples=model.corpus_count, epochs=model.iter)
+            with ph("save"):
+                model._sync_host()
+                if rank == 0:  # data parallel: the merged replicas are identical
+                    model.save(name)
+            if rank == 0:
+                # the text exports (generateMatrix.py, save_word2vec_format) read
+                # this iteration's checkpoint / tables only: they run on a host
+                # thread while the next iteration trains (one at a time, in order)
+                exporter.submit(name, model.wv, ph)
+            if world > 1:
+                import torch.distributed as dist
+                dist.barrier()  # the next iteration loads rank 0's checkpoint
+            print(f"gene2vec dimension {dimension} iteration {current_iter} done")
+            outputs.append(name)
+            del model
+    finally:
+        if pipe is not None:
+            pipe.close(wait=True)
     with ph("export_wait"):
         exporter.close()
     if args.timing and rank == 0:

@@ -156,6 +156,7 @@ class ShufflePipeline:
         self.perm, self.after, self.err = {}, {}, None
         self.k = 0
         self.dead = False
+        self.workers = []
         self.free = queue.Queue()
         for _ in range(depth):
             self.free.put(None)
@@ -177,8 +178,10 @@ class ShufflePipeline:
             buf = self.free.get()
             if self.dead:
                 return
-            threading.Thread(target=self._swaps, args=(k, st.copy(), pos.copy(), buf),
-                             daemon=True).start()
+            th = threading.Thread(target=self._swaps, args=(k, st.copy(), pos.copy(), buf),
+                                  daemon=True)
+            self.workers.append(th)
+            th.start()
             rc = L.g2v_py_shuffle_skip(N.ptr(st), N.ptr(pos), self.n)
             if rc != N.G2V_OK:
                 return self._fail(rc)
@@ -219,6 +222,12 @@ class ShufflePipeline:
         if not self.dead:
             self.free.put(perm)
 
-    def close(self):
+    def close(self, wait=False):
+        """stop drawing ahead; ``wait``: also join the threads (no native call
+        left running when the interpreter shuts down after an error)"""
         self.dead = True
         self.free.put(None)  # wakes a driver blocked on a buffer
+        if wait:
+            self.driver.join()
+            for th in list(self.workers):
+                th.join()

@@ -198,3 +198,11 @@ def test_pairs_permute_equals_csr_permute():
     np.testing.assert_array_equal(mixed.sent_off, [0, 3, 5])
     with pytest.raises(N.G2VError):
         Corpus(tok.copy(), off.copy(), [], None).permute_(np.full(n, n, dtype=np.int64))
+
+
+def test_shuffle_pipeline_close_wait_joins_threads():
+    pipe = ShufflePipeline(100003, random.Random(1), 4, depth=2)
+    pipe.next()
+    pipe.close(wait=True)
+    assert not pipe.driver.is_alive()
+    assert all(not t.is_alive() for t in pipe.workers)
