@@ -206,3 +206,25 @@ def test_shuffle_pipeline_close_wait_joins_threads():
     pipe.close(wait=True)
     assert not pipe.driver.is_alive()
     assert all(not t.is_alive() for t in pipe.workers)
+
+
+def test_adopt_vocab_ids_renumbers_corpus_once():
+    """gene2vec.py renumbers the corpus into the model's vocabulary order at
+    iteration 1 so later iterations skip the token remap"""
+    from gene2vec_amd.gene2vec import _adopt_vocab_ids
+    from gene2vec_amd.ingest import Corpus
+    c = Corpus(np.array([0, 1, 2, 0], np.int32), np.array([0, 2, 4], np.int64),
+               ["b", "a", "c"], np.array([2, 1, 1], np.int64))
+    ids = np.array([1, 0, 2], np.int32)  # corpus id -> model index
+    tok = ids[c.tokens]
+    _adopt_vocab_ids(c, ids, tok)
+    assert c.words == ["a", "b", "c"]
+    np.testing.assert_array_equal(c.tokens, [1, 0, 2, 1])
+    np.testing.assert_array_equal(c.counts, [1, 2, 1])
+    assert c.sentences() == [["b", "a"], ["c", "b"]]
+    # a word outside the vocabulary (-1) keeps the corpus numbering
+    d = Corpus(np.array([0, 1], np.int32), np.array([0, 2], np.int64), ["x", "y"],
+               np.array([1, 1], np.int64))
+    _adopt_vocab_ids(d, np.array([0, -1], np.int32), np.array([0, -1], np.int32))
+    assert d.words == ["x", "y"]
+    np.testing.assert_array_equal(d.tokens, [0, 1])
