@@ -10,8 +10,10 @@ i.e. downsampling + negative sampling + SGNS updates for every pair.  Inputs
 
 N > 1 (torchrun, one rank per GPU, RCCL over xGMI): weak scaling, each rank
 trains its own 125 M-pair shard (BASELINE configs[2]: 1 B pairs over 8 GPUs)
-on a replica of the tables, and the replicas are averaged with
-torch.distributed.all_reduce(AVG) every --avg-every-jobs jobs.
+on a replica of the tables, and every --avg-every-jobs jobs libg2v merges the
+replicas itself (g2v_average: fused HIP delta/apply kernels around one grouped
+ncclAllReduce on the training stream; torch.distributed only hands out the
+RCCL unique id).  N = 1 runs no merge at all.
 
 Prints ONE JSON line on rank 0 (see the contract in the task description):
 value = pairs/s over all ranks, plus `roofline` (dominant kernel =
@@ -57,7 +59,10 @@ def parse():
     p.add_argument("--seg-jobs", type=int, default=0,
                    help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
-    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="threads of the CPU baseline (0 = os.cpu_count(), every host core)")
+    p.add_argument("--cpu-extra", action="store_true",
+                   help="also time the CPU baseline on 1 core and on 16 threads")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-eval", action="store_true")
     p.add_argument("--no-gather-roof", action="store_true",
@@ -67,7 +72,7 @@ def parse():
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                         "the N>1 path with several ranks sharing one GPU)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return p.parse_args()
 
 
@@ -146,7 +151,15 @@ def main():
     rs = np.random.RandomState(Dd.rank_seed(1, rank))  # gensim model.random(seed=1) per rank
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
-    trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=a.merge)
+    merge_backend = "torch"
+    if world > 1 and a.backend == "nccl":
+        # libg2v's own RCCL communicator: rank 0's unique id over the process group
+        box = [eng.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(box, src=0)
+        eng.comm_init(box[0], world, rank)
+        merge_backend = "rccl"
+    trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=a.merge,
+                                backend=merge_backend)
     torch.cuda.synchronize(dev)
 
     def step(i, timing):
@@ -192,15 +205,20 @@ def main():
     alg_bytes_launch = st["examples"] * bytes_per_example / launches
     achieved = alg_bytes_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic = None
+    traffic_src = None
     if os.path.exists(a.traffic_json):
         try:
             tj = json.load(open(a.traffic_json))
             # per-example PMC bytes of the same workload (vocabulary, shape, downsampling
-            # and skew), scaled to this run's examples per launch
+            # and skew) from a separate rocprofv3 --pmc pass of this kernel, scaled to
+            # this run's examples per launch
             if (tj.get("vocab"), tj.get("dim"), tj.get("negative"), tj.get("sample"),
                     tj.get("zipf")) == (V0, D, K, a.sample, a.zipf):
                 traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
                                 * st["examples"] / launches, 1)
+                traffic_src = (f"{os.path.relpath(a.traffic_json, ROOT)}: PMC bytes per "
+                               f"example x this run's {st['examples'] // launches} examples "
+                               "per launch (not measured in this process)")
         except Exception:
             traffic = None
     atomic_bytes = (K + 2) * D * 4  # every SGNS update is a memory-side f32 atomic delta
@@ -214,7 +232,8 @@ def main():
                 "binding_resource": "memory-side float atomics (MI355X_MICROARCH.md: ~1300 GB/s "
                                     "of added bytes chip-wide)",
                 "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
-                "atomic_frac": round(atomic_gbps / 1300.0, 4)}
+                "atomic_frac": round(atomic_gbps / 1300.0, 4), "traffic_source": traffic_src,
+                "grid_workgroups": eng.get_option(N.OPT_GRID)}
 
     # ---- measured gather roof: the same kernel on the same index
     # stream with its table writes compiled out (G2V_OPT_DEBUG_WRITE=2) and a
@@ -254,23 +273,41 @@ def main():
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         from oracle import c_oracle as CO
-        ncpu = a.cpu_threads or min(16, os.cpu_count() or 1)
+        host_cores = os.cpu_count() or 1
+        ncpu = a.cpu_threads or host_cores
         ns = min(a.cpu_sample_pairs, n_pairs)
         jsc = E.plan_jobs(n_sent=ns, sent_len=2)
         off = np.arange(0, 2 * ns + 1, 2, dtype=np.int64)
-        c0 = syn0_h.copy()
-        c1 = np.zeros_like(c0)
         si = CO.sample_int(vcounts, a.sample)
         cum = CO.make_cum_table(vcounts)
         al = E.job_alphas(jsc, ns).astype(np.float32)
         sd = E.job_seeds(np.random.RandomState(1), len(jsc) - 1)
-        t = time.perf_counter()
-        CO.train(tok[:2 * ns], off, jsc, al, sd, si, a.sample != 0, cum, c0, c1,
-                 np.ones(V, np.float32), K, nthreads=ncpu)
-        dt = time.perf_counter() - t
+        ld_cpu = (D + 15) // 16 * 16  # rows on 64-B lines of their own (no false sharing)
+
+        def cpu_run(threads):
+            c0 = syn0_h.copy()
+            c1 = np.zeros_like(c0)
+            t = time.perf_counter()
+            CO.train(tok[:2 * ns], off, jsc, al, sd, si, a.sample != 0, cum, c0, c1,
+                     np.ones(V, np.float32), K, nthreads=threads, ld=ld_cpu)
+            return time.perf_counter() - t
+
+        dt = cpu_run(ncpu)
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except AttributeError:  # pragma: no cover
+            affinity = None
         cpu = {"value": round(ns / dt, 1), "unit": "pairs/s", "cores": ncpu, "kind": "port",
+               "host_cores": host_cores, "affinity_cores": affinity,
+               "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
                "sample": f"first {ns} pairs of the same corpus, 1 epoch, C oracle "
-                         f"(oracle/sgns_oracle.c) Hogwild OpenMP, {dt:.2f} s"}
+                         f"(oracle/sgns_oracle.c) Hogwild OpenMP on {ncpu} threads "
+                         f"(os.cpu_count() = {host_cores}), rows padded to {ld_cpu} floats, "
+                         f"{dt:.2f} s"}
+        if a.cpu_extra:
+            for th in (16, 1):
+                d = cpu_run(th)
+                cpu[f"value_{th}_threads"] = round(ns / d, 1)
 
     cfg_name = {(24447, 200, 5): "C2", (60000, 512, 15): "C4"}.get((V0, D, K), "custom")
     if rank == 0:

@@ -18,11 +18,17 @@ G2V_EHIP = -2
 G2V_ENOMEM = -3
 G2V_ESTATE = -4
 G2V_ERANGE = -5
+G2V_ECOMM = -6
+ABI_VERSION = 2
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
 MODE_MINIBATCH = 2
 FLAG_TIMING = 0x100
+FLAG_COMPUTE_LOSS = 0x200
+MERGE_TOUCH = 0
+MERGE_MEAN = 1
+UNIQUE_ID_BYTES = 128
 CORPUS_DEVICE = 0x1
 OPT_HOT_ROWS = 1
 OPT_CACHE_POLICY = 2
@@ -52,7 +58,8 @@ class G2VError(RuntimeError):
 class Stats(C.Structure):
     _fields_ = [("raw_words", C.c_int64), ("effective_words", C.c_int64),
                 ("examples", C.c_int64), ("jobs", C.c_int64), ("launches", C.c_int64),
-                ("sgns_kernel_ms", C.c_double), ("sample_kernel_ms", C.c_double)]
+                ("sgns_kernel_ms", C.c_double), ("sample_kernel_ms", C.c_double),
+                ("training_loss", C.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -73,6 +80,7 @@ SIGNATURES = {
     "g2v_destroy": (C.c_int, [_vp]),
     "g2v_set_stream": (C.c_int, [_vp, _vp]),
     "g2v_set_option": (C.c_int, [_vp, C.c_int, _i64]),
+    "g2v_get_option": (C.c_int, [_vp, C.c_int, C.POINTER(_i64)]),
     "g2v_row_stride": (C.c_int, [_vp, C.POINTER(_i64)]),
     "g2v_set_vocab": (C.c_int, [_vp, _vp, _f64, _f64, _vp, _vp]),
     "g2v_bind_tables": (C.c_int, [_vp, _vp, _vp, _i64]),
@@ -83,7 +91,13 @@ SIGNATURES = {
     "g2v_train": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _u32]),
     "g2v_sgns_step_explicit": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _f32, _u32]),
     "g2v_debug_sample": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, C.POINTER(_i64)]),
+    "g2v_reset_loss": (C.c_int, [_vp]),
     "g2v_sync": (C.c_int, [_vp]),
+    "g2v_comm_unique_id": (C.c_int, [_vp, _i64]),
+    "g2v_comm_init": (C.c_int, [_vp, _vp, C.c_int, C.c_int]),
+    "g2v_average": (C.c_int, [_vp, C.c_int]),
+    "g2v_merge_snapshot": (C.c_int, [_vp]),
+    "g2v_average_local": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_int]),
     "g2v_read_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "g2v_cosine_pairs": (C.c_int, [C.c_int, _vp, _i64, _i32, _vp, _vp, _i64, _vp]),
     "g2v_seeded_vectors": (C.c_int, [_vp, _i64, _i32, _vp]),
@@ -137,7 +151,7 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    if L.g2v_abi_version() != 1:
+    if L.g2v_abi_version() != ABI_VERSION:
         raise NativeLibraryError("libg2v ABI version mismatch")
     _lib = L
     return L

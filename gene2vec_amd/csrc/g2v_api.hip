@@ -4,14 +4,18 @@
 // ([ext] wv.vectors, trainables.syn1neg, trainables.vectors_lockf,
 // vocabulary.cum_table, per-word sample_int) and replaces the per-job hook
 // train_batch_sg that gensim's worker threads call (src/gene2vec.py:70,87).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: RCCL is dlopen()ed by g2v_comm_*
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <mutex>
 #include <new>
+#include <thread>
 #include <string>
 #include <utility>
 #include <vector>
@@ -96,6 +100,8 @@ struct g2v_ctx {
   int nv = 1, nvec = 0, rec_stride = 0;
   int64_t ld = 0;
   int cus = 0, sgns_grid = 0;
+  bool grid_user = false;       // G2V_OPT_GRID set explicitly
+  double u_max = 0.0;           // hottest-row updates per example (set_vocab)
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
@@ -150,8 +156,20 @@ struct g2v_ctx {
   int32_t* d_ex = nullptr;  // center | input | negs
   float *snap0 = nullptr, *snap1 = nullptr;
 
-  // counters: [0] effective words, [1] examples, [2] raw words
+  // counters: [0] effective words, [1] examples, [2] raw words, [3] fault bits
   unsigned long long* d_counters = nullptr;
+
+  // compute_loss: LOG_TABLE and the running loss ([0] double sum of the
+  // parallel modes; the float32 running sum of SEQUENTIAL lives in [1])
+  float* log_table = nullptr;
+  double* d_loss = nullptr;
+
+  // replica merge: snapshot of both tables at the last merge, touched-row counts
+  float *merge0 = nullptr, *merge1 = nullptr, *merge_cnt = nullptr;
+  int64_t merge_ld = 0;
+  bool merge_valid = false;
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
   int64_t jobs = 0, launches = 0;
 
   // timing
@@ -160,11 +178,24 @@ struct g2v_ctx {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> t_sgns, t_samp;
 };
 
-// Hogwild staleness bound: with more than ~2k waves in flight the summed
-// stale updates of the hottest rows destabilise SGD (measured at V=24447:
-// 512 workgroups track the sequential oracle, 1024 diverge in iteration 1).
-static int default_grid(int cus, int K, int nv) {
-  return std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
+// Hogwild staleness bound.  Every wave in flight holds one example whose
+// updates the others do not see yet; the rows that suffer are the hottest
+// syn1neg rows, which take u_max = max_r(K p_neg(r) + p_tok(r)) updates per
+// example (p_neg: the unigram^0.75 table, p_tok: the downsampled token
+// distribution).  Measured: 2 workgroups (8 waves) per CU track the sequential
+// oracle at C2 (V 24,447 Zipf, u_max 0.12) and at C4 (V 60,000, K 15, u_max
+// 0.27) through the 10-iteration schedule, while 3 per CU diverge at C2.  So
+// the grid is 2 workgroups per CU, cut further where a vocabulary is hotter
+// than C4: waves x u_max <= kStaleBudget (= 2,048 waves x 0.267).
+constexpr double kStaleBudget = 546.0;
+
+static int default_grid(int cus, int K, int nv, double u_max) {
+  int g = std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
+  if (u_max > 0.0) {
+    const int waves = (int)(kStaleBudget / u_max);
+    g = std::min(g, std::max(1, waves / (kSgnsThreads / 64)));
+  }
+  return g;
 }
 
 static int ctx_event(g2v_ctx* c, hipEvent_t* out) {
@@ -181,6 +212,88 @@ static int set_dev(g2v_ctx* c) {
   REQUIRE(c != nullptr, G2V_EINVAL, "null context");
   HIPCHK(hipSetDevice(c->device));
   return G2V_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL, loaded at run time: a process that imported torch already holds
+// torch's librccl.so.1 (same soname), and dlopen returns that copy, so the
+// process has one RCCL; without torch the ROCm copy is loaded.
+// ---------------------------------------------------------------------------
+namespace {
+struct Rccl {
+  decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+  decltype(&ncclCommInitRank) comm_init_rank = nullptr;
+  decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  std::string load_error;
+};
+
+const Rccl& rccl() {
+  static Rccl r;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!h) {
+      const char* e = dlerror();
+      r.load_error = std::string("dlopen(librccl.so.1) failed: ") + (e ? e : "?");
+      return;
+    }
+    bool ok = true;
+    auto sym = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      ok = ok && fn != nullptr;
+    };
+    sym(r.get_unique_id, "ncclGetUniqueId");
+    sym(r.comm_init_rank, "ncclCommInitRank");
+    sym(r.comm_destroy, "ncclCommDestroy");
+    sym(r.all_reduce, "ncclAllReduce");
+    sym(r.broadcast, "ncclBroadcast");
+    sym(r.group_start, "ncclGroupStart");
+    sym(r.group_end, "ncclGroupEnd");
+    sym(r.error_string, "ncclGetErrorString");
+    if (!ok) {
+      r.get_unique_id = nullptr;
+      r.load_error = "librccl.so.1 lacks an nccl* entry point";
+    }
+  });
+  return r;
+}
+
+int rccl_fail(ncclResult_t e, const char* what) {
+  const Rccl& r = rccl();
+  return fail(G2V_ECOMM, "%s failed: %s", what, r.error_string ? r.error_string(e) : "?");
+}
+}  // namespace
+
+#define NCCLCHK(x, what)                           \
+  do {                                             \
+    ncclResult_t e_ = (x);                         \
+    if (e_ != ncclSuccess) return rccl_fail(e_, what); \
+  } while (0)
+
+static void comm_destroy(g2v_ctx* c) {
+  if (c->comm && rccl().comm_destroy) (void)rccl().comm_destroy(c->comm);
+  c->comm = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+}
+
+// device fault latched by the sampler (counters[3]); reads and clears it
+static int check_fault(g2v_ctx* c) {
+  unsigned long long f = 0;
+  HIPCHK(hipMemcpy(&f, c->d_counters + 3, sizeof f, hipMemcpyDeviceToHost));
+  if (!f) return G2V_OK;
+  HIPCHK(hipMemset(c->d_counters + 3, 0, sizeof f));
+  std::string m = "device corpus fault:";
+  if (f & kFaultTokenRange) m += " token id outside [-1, V) (skipped as out of vocabulary);";
+  if (f & kFaultJobSize) m += " job of several sentences holds > 10000 raw words (not trained);";
+  return fail(G2V_EINVAL, "%s", m.c_str());
 }
 
 extern "C" {
@@ -234,7 +347,7 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
   if (hipGetDeviceProperties(&prop, device) != hipSuccess)
     return bail(fail(G2V_EHIP, "hipGetDeviceProperties failed"));
   c->cus = prop.multiProcessorCount;
-  c->sgns_grid = default_grid(c->cus, negative, nv);
+  c->sgns_grid = default_grid(c->cus, negative, nv, 0.0);
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(G2V_EHIP, "hipStreamCreate failed"));
   c->stream = c->own_stream;
@@ -250,22 +363,27 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
       (rc = dev_alloc(&c->sample_int, (size_t)c->V)) ||
       (rc = dev_alloc(&c->bkt, (size_t)kBuckets + 1)) ||
       (rc = dev_alloc(&c->d_counts, (size_t)c->V)) || (rc = dev_alloc(&c->d_cpow, (size_t)c->V)) ||
-      (rc = dev_alloc(&c->d_counters, 4)))
+      (rc = dev_alloc(&c->d_counters, 4)) || (rc = dev_alloc(&c->log_table, kExpTableSize)) ||
+      (rc = dev_alloc(&c->d_loss, 2)))
     return bail(rc);
   c->syn0 = c->own0;
   c->syn1 = c->own1;
 
-  // constant tables: sigmoid LUT ([ext] init()) and LCG jump tables, built on host
-  float lut[kExpTableSize];
+  // constant tables: sigmoid LUT and LOG_TABLE ([ext] init(): LOG_TABLE[i] =
+  // <REAL_t>log(EXP_TABLE[i])) and LCG jump tables, built on host
+  float lut[kExpTableSize], logt[kExpTableSize];
   for (int i = 0; i < kExpTableSize; ++i) {
     const float x = ((float)i / (float)kExpTableSize * 2 - 1) * kMaxExp;
     const float e = (float)exp((double)x);
     lut[i] = e / (e + 1);
+    logt[i] = (float)log((double)lut[i]);
   }
   std::vector<uint64_t> jt(4 * (size_t)kJumpTab);
   lcg_jump_tables(jt.data(), jt.data() + kJumpTab, jt.data() + 2 * kJumpTab,
                   jt.data() + 3 * kJumpTab);
   if (hipMemcpy(c->exp_table, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->log_table, logt, sizeof logt, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(c->d_loss, 0, 2 * sizeof(double)) != hipSuccess ||
       hipMemcpy(c->jump, jt.data(), jt.size() * sizeof(uint64_t), hipMemcpyHostToDevice) !=
           hipSuccess ||
       hipMemset(c->own0, 0, tab * sizeof(float)) != hipSuccess ||
@@ -306,6 +424,12 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->snap0);
   dev_free(c->snap1);
   dev_free(c->d_counters);
+  dev_free(c->log_table);
+  dev_free(c->d_loss);
+  dev_free(c->merge0);
+  dev_free(c->merge1);
+  dev_free(c->merge_cnt);
+  comm_destroy(c);
   dev_free(c->stripe);
   dev_free(c->dbg16);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -376,10 +500,25 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       return G2V_OK;
     case G2V_OPT_GRID:
       REQUIRE(value >= 0, G2V_EINVAL, "grid must be >= 0");
-      c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv);
+      c->grid_user = value > 0;
+      c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv, c->u_max);
       return G2V_OK;
     default:
       return fail(G2V_EINVAL, "unknown option key %d", key);
+  }
+}
+
+int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
+  REQUIRE(c && out, G2V_EINVAL, "null argument");
+  switch (key) {
+    case G2V_OPT_HOT_ROWS: *out = c->hot_rows; return G2V_OK;
+    case G2V_OPT_CACHE_POLICY: *out = c->cache_policy; return G2V_OK;
+    case G2V_OPT_SEG_JOBS: *out = c->seg_jobs; return G2V_OK;
+    case G2V_OPT_GRID: *out = c->sgns_grid; return G2V_OK;
+    case G2V_OPT_DEBUG_WRITE: *out = c->debug_write; return G2V_OK;
+    case G2V_OPT_STRIPE_ROWS: *out = c->stripe_rows; return G2V_OK;
+    case G2V_OPT_STRIPE_COPIES: *out = c->stripe_copies; return G2V_OK;
+    default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
 
@@ -397,6 +536,25 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
   REQUIRE(sample >= 0.0, G2V_EINVAL, "sample must be >= 0");
   for (int32_t i = 0; i < c->V; ++i)
     REQUIRE(counts[i] > 0, G2V_EINVAL, "counts[%d] = %lld must be > 0", i, (long long)counts[i]);
+  {
+    // staleness budget of the Hogwild grid (default_grid)
+    double tot = 0.0, zn = 0.0, zt = 0.0;
+    for (int32_t i = 0; i < c->V; ++i) tot += (double)counts[i];
+    const double thr = sample == 0.0 ? 0.0 : (sample < 1.0 ? sample * tot : sample * 2.618);
+    std::vector<double> pt((size_t)c->V), pn((size_t)c->V);
+    for (int32_t i = 0; i < c->V; ++i) {
+      const double v = (double)counts[i];
+      const double keep = thr > 0.0 ? std::min(1.0, (sqrt(v / thr) + 1.0) * (thr / v)) : 1.0;
+      pt[i] = v * keep;
+      pn[i] = pow(v, ns_exponent);
+      zt += pt[i];
+      zn += pn[i];
+    }
+    double um = 0.0;
+    for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn + pt[i] / zt);
+    c->u_max = um;
+    if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
+  }
   HIPCHK(hipMemcpyAsync(c->d_counts, counts, sizeof(int64_t) * c->V, hipMemcpyHostToDevice,
                         c->stream));
   HIPCHK(launch_vocab(c->d_counts, c->d_cpow, c->V, ns_exponent, sample, c->cum, c->sample_int,
@@ -435,6 +593,7 @@ int g2v_bind_tables(g2v_ctx* c, float* s0, float* s1, int64_t ld) {
   c->syn1 = s1;
   c->ld = ld;
   c->weights_ready = true;
+  if (c->merge_valid) return g2v_merge_snapshot(c);
   return G2V_OK;
 }
 
@@ -454,6 +613,7 @@ int g2v_set_weights(g2v_ctx* c, const float* s0, const float* s1, const float* l
     HIPCHK(hipMemcpyAsync(c->lockf, lockf, sizeof(float) * c->V, hipMemcpyHostToDevice, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));  // host buffers are only borrowed for the call
   c->weights_ready = true;
+  if (c->merge_valid) return g2v_merge_snapshot(c);
   return G2V_OK;
 }
 
@@ -468,6 +628,33 @@ int g2v_get_weights(g2v_ctx* c, float* s0, float* s1) {
   HIPCHK(hipStreamSynchronize(c->stream));
   return G2V_OK;
 }
+
+}  // extern "C"
+
+// min / max of n int32 ids (host corpus check, parallel over up to 8 threads)
+static void id_range(const int32_t* x, int64_t n, int32_t* lo, int32_t* hi) {
+  const int64_t kGrain = 1 << 22;
+  const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, n / kGrain));
+  std::vector<int32_t> mn(nt, INT32_MAX), mx(nt, INT32_MIN);
+  auto run = [&](int k) {
+    const int64_t b = n * k / nt, e = n * (k + 1) / nt;
+    int32_t a = INT32_MAX, z = INT32_MIN;
+    for (int64_t i = b; i < e; ++i) {
+      a = std::min(a, x[i]);
+      z = std::max(z, x[i]);
+    }
+    mn[k] = a;
+    mx[k] = z;
+  };
+  std::vector<std::thread> th;
+  for (int k = 1; k < nt; ++k) th.emplace_back(run, k);
+  run(0);
+  for (auto& t : th) t.join();
+  *lo = *std::min_element(mn.begin(), mn.end());
+  *hi = *std::max_element(mx.begin(), mx.end());
+}
+
+extern "C" {
 
 int g2v_set_corpus(g2v_ctx* c, const int32_t* tokens, int64_t n_tokens, const int64_t* sent_off,
                    int64_t n_sent, int64_t sent_len, uint32_t flags) {
@@ -491,14 +678,25 @@ int g2v_set_corpus(g2v_ctx* c, const int32_t* tokens, int64_t n_tokens, const in
     c->tok = tokens;
     c->sent_off = sent_len > 0 ? nullptr : sent_off;
   } else {
+    if (n_tokens > 0) {
+      int32_t lo, hi;
+      id_range(tokens, n_tokens, &lo, &hi);
+      REQUIRE(lo >= -1 && hi < c->V, G2V_EINVAL,
+              "corpus ids must lie in [-1, V=%d) (found [%d, %d])", c->V, lo, hi);
+    }
+    if (sent_len <= 0) {
+      REQUIRE(sent_off[0] == 0 && sent_off[n_sent] == n_tokens, G2V_EINVAL,
+              "sent_off must start at 0 and end at n_tokens");
+      for (int64_t i = 0; i < n_sent; ++i)
+        REQUIRE(sent_off[i + 1] >= sent_off[i], G2V_EINVAL, "sent_off decreases at %lld",
+                (long long)i);
+    }
     if ((rc = dev_alloc(&c->own_tok, (size_t)n_tokens))) return rc;
     HIPCHK(hipMemcpy(c->own_tok, tokens, sizeof(int32_t) * n_tokens, hipMemcpyHostToDevice));
     c->tok = c->own_tok;
     if (sent_len > 0) {
       c->sent_off = nullptr;
     } else {
-      REQUIRE(sent_off[0] == 0 && sent_off[n_sent] == n_tokens, G2V_EINVAL,
-              "sent_off must start at 0 and end at n_tokens");
       if ((rc = dev_alloc(&c->own_off, (size_t)n_sent + 1))) return rc;
       HIPCHK(hipMemcpy(c->own_off, sent_off, sizeof(int64_t) * (n_sent + 1),
                        hipMemcpyHostToDevice));
@@ -565,9 +763,12 @@ static int check_jobs(const g2v_ctx* c, const int64_t* job_sent, int64_t n_jobs)
             G2V_EINVAL, "job %lld sentence range [%lld, %lld) invalid (n_sent=%lld)",
             (long long)j, (long long)job_sent[j], (long long)job_sent[j + 1],
             (long long)c->n_sent);
+    // [ext] _job_producer gives a sentence over batch_words a job of its own;
+    // train_batch_sg truncates it at 10000 effective words
     const int64_t nt = tokens_between(c, job_sent[j], job_sent[j + 1]);
-    REQUIRE(nt <= kBatchWords, G2V_ERANGE, "job %lld holds %lld raw words > batch_words %d",
-            (long long)j, (long long)nt, kBatchWords);
+    REQUIRE(nt <= kBatchWords || job_sent[j + 1] - job_sent[j] == 1, G2V_ERANGE,
+            "job %lld holds %lld raw words in %lld sentences > batch_words %d", (long long)j,
+            (long long)nt, (long long)(job_sent[j + 1] - job_sent[j]), kBatchWords);
   }
   return G2V_OK;
 }
@@ -583,7 +784,7 @@ static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing) {
   // (job_sent lives in pinned staging, still valid: read it from there)
   const int64_t* hjs = (const int64_t*)c->h_stage;
   const int64_t tk = tokens_between(c, hjs[j0], hjs[j0 + nj]);
-  if (tk >= 0) max_ex = std::max<int64_t>(2 * tk, 1);
+  if (tk >= 0) max_ex = std::max<int64_t>(2 * std::min<int64_t>(tk, nj * (int64_t)kBatchWords), 1);
   if ((rc = dev_reserve(c->stream, &c->d_rec, &c->rec_cap, max_ex * c->rec_stride))) return rc;
 
   SampleArgs a{};
@@ -622,7 +823,7 @@ static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing) {
 }
 
 static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool timing,
-                    const float* rd0, const float* rd1) {
+                    bool closs, const float* rd0, const float* rd1) {
   SgnsArgs s{};
   s.rec = c->d_rec;
   s.rec_stride = c->rec_stride;
@@ -639,6 +840,10 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.hot_rows = c->hot_rows < 0 ? c->V : std::min(c->hot_rows, c->V);
   s.exp_table = c->exp_table;
   s.debug_write = c->debug_write;
+  s.compute_loss = closs ? 1 : 0;
+  s.log_table = c->log_table;
+  s.loss_f64 = c->d_loss;
+  s.loss_f32 = reinterpret_cast<float*>(c->d_loss + 1);
   const bool atomic_kernel = mode == kModeHogwild && s.hot_rows >= c->V;
   const bool striped = atomic_kernel && c->stripe_copies > 1 && c->stripe_rows > 0;
   s.stripe_rows = striped ? std::min(c->stripe_rows, c->V) : 0;
@@ -687,9 +892,18 @@ int g2v_plan_jobs(const int64_t* sent_off, int64_t n_sent, int64_t sent_len, int
     // fixed-length sentences: the loop below packs exactly
     // floor(batch_words / sent_len) sentences per job, so the starts are a
     // closed form (no O(n_sent) pass per train() call: 100 M pairs cost 73 ms)
-    REQUIRE(n_sent == 0 || sent_len <= batch_words, G2V_ERANGE,
-            "sentence 0 has %lld tokens > batch_words %lld (unsupported)", (long long)sent_len,
-            (long long)batch_words);
+    if (sent_len > batch_words && n_sent > 0) {
+      // every sentence overflows a job: the producer first queues the empty
+      // job, then each sentence alone -> {0, 0, 1, ..., n_sent}
+      const int64_t nj = n_sent + 1;
+      if (job_sent)
+        for (int64_t j = 0; j <= nj && j < cap; ++j) job_sent[j] = j == 0 ? 0 : j - 1;
+      *n_jobs_out = nj;
+      if (job_sent && cap < nj + 1)
+        return fail(G2V_ERANGE, "job_sent capacity %lld < %lld", (long long)cap,
+                    (long long)(nj + 1));
+      return G2V_OK;
+    }
     const int64_t per = n_sent ? batch_words / sent_len : 1;
     const int64_t nj = (n_sent + per - 1) / per;
     if (job_sent)
@@ -706,9 +920,6 @@ int g2v_plan_jobs(const int64_t* sent_off, int64_t n_sent, int64_t sent_len, int
   };
   for (int64_t i = 0; i < n_sent; ++i) {
     const int64_t ln = sent_len > 0 ? sent_len : sent_off[i + 1] - sent_off[i];
-    REQUIRE(ln <= batch_words, G2V_ERANGE,
-            "sentence %lld has %lld tokens > batch_words %lld (unsupported)", (long long)i,
-            (long long)ln, (long long)batch_words);
     if (size + ln <= batch_words) {
       size += ln;
     } else {
@@ -738,11 +949,12 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
   if ((rc = check_jobs(c, job_sent, n_jobs))) return rc;
   if (n_jobs == 0) return G2V_OK;
   const bool timing = flags & G2V_FLAG_TIMING;
+  const bool closs = flags & G2V_FLAG_COMPUTE_LOSS;
   if ((rc = upload_jobs(c, job_sent, job_alpha, job_seed, n_jobs))) return rc;
   for (int64_t j0 = 0; j0 < n_jobs; j0 += c->seg_jobs) {
     const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
     if ((rc = sample_segment(c, j0, nj, timing))) return rc;
-    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, c->syn0, c->syn1))) return rc;
+    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, closs, c->syn0, c->syn1))) return rc;
   }
   c->jobs += n_jobs;
   return G2V_OK;
@@ -826,7 +1038,9 @@ int g2v_sgns_step_explicit(g2v_ctx* c, const int32_t* center, const int32_t* inp
     rd0 = c->snap0;
     rd1 = c->snap1;
   }
-  if ((rc = run_sgns(c, c->d_job_exoff, mode, flags & G2V_FLAG_TIMING, rd0, rd1))) return rc;
+  if ((rc = run_sgns(c, c->d_job_exoff, mode, flags & G2V_FLAG_TIMING,
+                     flags & G2V_FLAG_COMPUTE_LOSS, rd0, rd1)))
+    return rc;
   // host arrays were copied asynchronously from pageable memory: finish before returning
   HIPCHK(hipStreamSynchronize(c->stream));
   return G2V_OK;
@@ -864,6 +1078,13 @@ int g2v_sync(g2v_ctx* c) {
   int rc = set_dev(c);
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->stream));
+  return check_fault(c);
+}
+
+int g2v_reset_loss(g2v_ctx* c) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(c->d_loss, 0, 2 * sizeof(double), c->stream));
   return G2V_OK;
 }
 
@@ -872,11 +1093,17 @@ int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
   if (rc) return rc;
   REQUIRE(out != nullptr, G2V_EINVAL, "out is null");
   HIPCHK(hipStreamSynchronize(c->stream));
+  if ((rc = check_fault(c))) return rc;
   unsigned long long cnt[4] = {0, 0, 0, 0};
+  double loss[2] = {0.0, 0.0};
   HIPCHK(hipMemcpy(cnt, c->d_counters, sizeof cnt, hipMemcpyDeviceToHost));
+  HIPCHK(hipMemcpy(loss, c->d_loss, sizeof loss, hipMemcpyDeviceToHost));
   HIPCHK(hipMemsetAsync(c->d_counters, 0, sizeof cnt, c->stream));
   HIPCHK(hipStreamSynchronize(c->stream));
   memset(out, 0, sizeof *out);
+  float lf32;
+  memcpy(&lf32, &loss[1], sizeof lf32);
+  out->training_loss = loss[0] + (double)lf32;
   out->effective_words = (int64_t)cnt[0];
   out->examples = (int64_t)cnt[1];
   out->raw_words = (int64_t)cnt[2];
@@ -897,6 +1124,134 @@ int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
   c->ev_used = 0;
   c->jobs = 0;
   c->launches = 0;
+  return G2V_OK;
+}
+
+// ---------------------------------------------------------------------------
+// multi-GPU replica averaging
+// ---------------------------------------------------------------------------
+int g2v_comm_unique_id(void* id_out, int64_t id_bytes) {
+  REQUIRE(id_out != nullptr && id_bytes >= (int64_t)sizeof(ncclUniqueId), G2V_EINVAL,
+          "id buffer must hold %zu bytes", sizeof(ncclUniqueId));
+  const Rccl& r = rccl();
+  REQUIRE(r.get_unique_id != nullptr, G2V_ECOMM, "RCCL unavailable: %s", r.load_error.c_str());
+  ncclUniqueId id;
+  NCCLCHK(r.get_unique_id(&id), "ncclGetUniqueId");
+  memcpy(id_out, &id, sizeof id);
+  return G2V_OK;
+}
+
+int g2v_merge_snapshot(g2v_ctx* c) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(c->weights_ready, G2V_ESTATE, "tables must be set or bound before a merge snapshot");
+  const size_t tab = (size_t)c->V * (size_t)c->ld;
+  if (!c->merge0 || c->merge_ld != c->ld) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    dev_free(c->merge0);
+    dev_free(c->merge1);
+    dev_free(c->merge_cnt);
+    if ((rc = dev_alloc(&c->merge0, tab)) || (rc = dev_alloc(&c->merge1, tab)) ||
+        (rc = dev_alloc(&c->merge_cnt, 2 * (size_t)c->V)))
+      return rc;
+    c->merge_ld = c->ld;
+  }
+  HIPCHK(hipMemcpyAsync(c->merge0, c->syn0, tab * sizeof(float), hipMemcpyDeviceToDevice,
+                        c->stream));
+  HIPCHK(hipMemcpyAsync(c->merge1, c->syn1, tab * sizeof(float), hipMemcpyDeviceToDevice,
+                        c->stream));
+  c->merge_valid = true;
+  return G2V_OK;
+}
+
+int g2v_comm_init(g2v_ctx* c, const void* id, int nranks, int rank) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(id != nullptr, G2V_EINVAL, "rccl_unique_id is null");
+  REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, G2V_EINVAL, "rank %d of %d invalid", rank,
+          nranks);
+  REQUIRE(c->weights_ready, G2V_ESTATE, "set or bind the tables before g2v_comm_init");
+  const Rccl& r = rccl();
+  REQUIRE(r.comm_init_rank != nullptr, G2V_ECOMM, "RCCL unavailable: %s", r.load_error.c_str());
+  comm_destroy(c);
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof uid);
+  ncclComm_t comm = nullptr;
+  NCCLCHK(r.comm_init_rank(&comm, nranks, uid, rank), "ncclCommInitRank");
+  c->comm = comm;
+  c->nranks = nranks;
+  c->rank = rank;
+  // every replica starts from rank 0's tables (Python's hash() seeds the
+  // reference's init differently in every process)
+  const size_t tab = (size_t)c->V * (size_t)c->ld;
+  if (nranks > 1) {
+    NCCLCHK(r.group_start(), "ncclGroupStart");
+    NCCLCHK(r.broadcast(c->syn0, c->syn0, tab, ncclFloat32, 0, comm, c->stream), "ncclBroadcast");
+    NCCLCHK(r.broadcast(c->syn1, c->syn1, tab, ncclFloat32, 0, comm, c->stream), "ncclBroadcast");
+    NCCLCHK(r.group_end(), "ncclGroupEnd");
+  }
+  return g2v_merge_snapshot(c);
+}
+
+int g2v_average(g2v_ctx* c, int rule) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %d", rule);
+  if (!c->comm) return G2V_OK;  // one rank: the full path runs (an identity on the values)
+  REQUIRE(c->merge_valid && c->merge_ld == c->ld, G2V_ESTATE,
+          "no merge snapshot (g2v_comm_init / g2v_merge_snapshot)");
+  const Rccl& r = rccl();
+  const size_t tab = (size_t)c->V * (size_t)c->ld;
+  float* t[2] = {c->syn0, c->syn1};
+  float* o[2] = {c->merge0, c->merge1};
+  if (rule == G2V_MERGE_TOUCH)
+    for (int k = 0; k < 2; ++k)
+      HIPCHK(launch_merge_delta(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
+                                c->stream));
+  NCCLCHK(r.group_start(), "ncclGroupStart");
+  for (int k = 0; k < 2; ++k)
+    NCCLCHK(r.all_reduce(t[k], t[k], tab, ncclFloat32, ncclSum, c->comm, c->stream),
+            "ncclAllReduce");
+  if (rule == G2V_MERGE_TOUCH)
+    NCCLCHK(r.all_reduce(c->merge_cnt, c->merge_cnt, 2 * (size_t)c->V, ncclFloat32, ncclSum,
+                         c->comm, c->stream),
+            "ncclAllReduce");
+  NCCLCHK(r.group_end(), "ncclGroupEnd");
+  for (int k = 0; k < 2; ++k)
+    HIPCHK(launch_merge_apply(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
+                              rule, 1.0f / (float)c->nranks, c->stream));
+  return G2V_OK;
+}
+
+int g2v_average_local(g2v_ctx* const* ctxs, int n, int rule) {
+  REQUIRE(ctxs != nullptr && n >= 1 && n <= kMaxLocalReplicas, G2V_EINVAL,
+          "need 1..%d contexts", kMaxLocalReplicas);
+  REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %d", rule);
+  g2v_ctx* c0 = ctxs[0];
+  int rc = set_dev(c0);
+  if (rc) return rc;
+  LocalMergeArgs a{};
+  for (int i = 0; i < n; ++i) {
+    g2v_ctx* c = ctxs[i];
+    REQUIRE(c != nullptr, G2V_EINVAL, "context %d is null", i);
+    REQUIRE(c->device == c0->device && c->V == c0->V && c->D == c0->D && c->ld == c0->ld,
+            G2V_EINVAL, "context %d differs in device / V / D / ld", i);
+    REQUIRE(c->merge_valid && c->merge_ld == c->ld, G2V_ESTATE,
+            "context %d has no merge snapshot (g2v_merge_snapshot)", i);
+    // the merge reads every replica: their queued work must be done
+    if (c->stream != c0->stream) HIPCHK(hipStreamSynchronize(c->stream));
+  }
+  for (int k = 0; k < 2; ++k) {
+    for (int i = 0; i < n; ++i) {
+      a.t[i] = k ? ctxs[i]->syn1 : ctxs[i]->syn0;
+      a.old[i] = k ? ctxs[i]->merge1 : ctxs[i]->merge0;
+    }
+    HIPCHK(launch_merge_local(a, n, c0->V, c0->ld, c0->nvec, rule, c0->stream));
+  }
+  // later work on the other contexts' streams must see the merged tables
+  bool other = false;
+  for (int i = 1; i < n; ++i) other |= ctxs[i]->stream != c0->stream;
+  if (other) HIPCHK(hipStreamSynchronize(c0->stream));
   return G2V_OK;
 }
 

@@ -23,6 +23,16 @@ __device__ __forceinline__ uint64_t lcg_jump(uint64_t s, uint32_t n, const LcgJu
   return s;
 }
 
+// any n >= 0: whole 2**22-step strides first (only a single sentence far
+// longer than batch_words, heavily downsampled, draws that many)
+__device__ __forceinline__ uint64_t lcg_jump_big(uint64_t s, uint64_t n, const LcgJump& j) {
+  while (n >= kMaxJump) {
+    s = lcg_step(lcg_jump(s, kMaxJump - 1, j));
+    n -= kMaxJump;
+  }
+  return lcg_jump(s, (uint32_t)n, j);
+}
+
 // bisect_left(cum, x, 0, V) restricted to the bucket that holds x
 __device__ __forceinline__ int32_t bisect_bucket(const uint32_t* __restrict__ cum,
                                                  const int32_t* __restrict__ bkt, int32_t V,

@@ -59,8 +59,13 @@ struct SampleArgs {
   int32_t* job_nex;         // [seg jobs]
   const int64_t* job_exoff; // [seg jobs + 1]
   int32_t* rec;
-  unsigned long long* counters;  // [0] effective words, [1] examples, [2] raw words
+  unsigned long long* counters;  // [0] effective words, [1] examples, [2] raw words,
+                                 // [3] fault bits (kFault*)
 };
+
+// sampler fault bits (counters[3]), reported by g2v_sync / g2v_read_stats
+constexpr unsigned long long kFaultTokenRange = 1;  // corpus id outside [-1, V)
+constexpr unsigned long long kFaultJobSize = 2;     // multi-sentence job > kBatchWords raw words
 
 struct SgnsArgs {
   const int32_t* rec;       // [E][rec_stride]: center, input, alpha bits, negs[K]
@@ -85,6 +90,11 @@ struct SgnsArgs {
   int stripe_rows;
   int stripe_copies;        // 1 = off
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]
+  // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
+  int compute_loss;
+  const float* log_table;   // [1000] (float)log(EXP_TABLE[i])
+  float* loss_f32;          // sequential: gensim's float32 running sum, continued
+  double* loss_f64;         // parallel modes: per-wave float partials summed in double
 };
 
 hipError_t launch_job_sample(bool write, const SampleArgs& a, int64_t n_jobs, hipStream_t st);
@@ -112,6 +122,21 @@ hipError_t launch_sgns_atomic(const SgnsArgs& a, int K, int nv, int grid, hipStr
 int sgns_blocks_per_cu(int K, int nv);
 hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
                                int64_t ld, int nvec, hipStream_t st);
+// replica merge (g2v_average*): rows of one [V][ld] table per call
+//   delta:  t <- t - old; cnt[row] = any(t - old != 0)
+//   apply:  touch: old <- old + t / max(cnt, 1); mean: old <- t * inv_n;  t <- old
+//   local:  the whole touch/mean merge over n replicas of one device
+constexpr int kMaxLocalReplicas = 16;
+struct LocalMergeArgs {
+  float* t[kMaxLocalReplicas];
+  float* old[kMaxLocalReplicas];
+};
+hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V, int64_t ld,
+                              int nvec, hipStream_t st);
+hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V, int64_t ld,
+                              int nvec, int rule, float inv_n, hipStream_t st);
+hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
+                              int rule, hipStream_t st);
 hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const int32_t* a,
                                const int32_t* b, int64_t n, float* out, hipStream_t st);
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,

@@ -32,46 +32,69 @@ namespace g2v {
 // ---------------------------------------------------------------------------
 // k_job_sample: one workgroup per job ([ext] train_batch_sg pre-pass)
 // ---------------------------------------------------------------------------
+//
+// gensim's train_batch_sg stops collecting at MAX_SENTENCE_LEN = 10000
+// effective words (the token that makes the 10000th kept word is the last one
+// that draws).  g2v_plan_jobs gives a sentence longer than batch_words a job of
+// its own, so a job of n > kBatchWords raw words is one sentence: its kept
+// prefix is collected chunk by chunk and the scan stops at the cut.
 template <bool WRITE>
 __global__ __launch_bounds__(kSampleThreads) void k_job_sample(SampleArgs a) {
   __shared__ int32_t s_eff[kBatchWords];       // kept tokens, compacted
-  __shared__ uint16_t s_kc[kBatchWords + 1];   // kept-before count per raw position
+  __shared__ uint16_t s_kc[kBatchWords];       // kept-before count per raw position
   __shared__ int s_scan[kSampleThreads / 64];
+  __shared__ long long s_cut_draws;            // draws up to the 10000th kept word, -1 = no cut
+  __shared__ int s_bad;
 
   const int64_t j = blockIdx.x;                // job within segment
   const int64_t jg = a.job0 + j;
   const int64_t s0 = a.job_sent[jg], s1 = a.job_sent[jg + 1];
   const int64_t tb = sent_start(a, s0);
-  const int n = (int)(sent_start(a, s1) - tb);  // <= kBatchWords (host-checked)
+  const int64_t n_raw = sent_start(a, s1) - tb;
+  const int ns_raw = (int)(s1 - s0);
+  // more than kBatchWords raw words in several sentences cannot come from
+  // g2v_plan_jobs (a host CSR is checked; a device CSR is not): train nothing
+  const bool bad_job = n_raw > kBatchWords && ns_raw > 1;
+  const int64_t n = bad_job ? 0 : n_raw;
+  const int ns = bad_job ? 0 : ns_raw;
   const uint64_t seed = a.job_seed[jg];
+  if (threadIdx.x == 0) {
+    s_cut_draws = -1;
+    s_bad = 0;
+  }
+  __syncthreads();
 
-  int inv_base = 0, keep_base = 0;
-  for (int t0 = 0; t0 < n; t0 += kSampleThreads) {
-    const int t = t0 + threadIdx.x;
-    const int32_t w = (t < n) ? a.tok[tb + t] : -1;
+  int64_t inv_base = 0;
+  int keep_base = 0;
+  for (int64_t t0 = 0; t0 < n && keep_base < kBatchWords; t0 += kSampleThreads) {
+    const int64_t t = t0 + threadIdx.x;
+    int32_t w = (t < n) ? a.tok[tb + t] : -1;
+    if (w < -1 || w >= a.V) {  // not a vocabulary index: skipped like OOV, reported
+      s_bad = 1;
+      w = -1;
+    }
     const int inv = (w >= 0);
     int tot_inv;
-    const int p = inv_base + block_excl_scan<kSampleThreads>(inv, s_scan, tot_inv);
+    const int64_t p = inv_base + block_excl_scan<kSampleThreads>(inv, s_scan, tot_inv);
     int keep = inv;
     if (inv && a.sample_on) {
       // gensim: drop iff sample_int < random_int32(&next_random); the p-th draw
-      const uint32_t r = (uint32_t)(lcg_jump(seed, (uint32_t)p, a.jump) >> 16);
+      const uint32_t r = (uint32_t)(lcg_jump_big(seed, (uint64_t)p, a.jump) >> 16);
       keep = !(a.sample_int[w] < r);
     }
     int tot_keep;
     const int c = keep_base + block_excl_scan<kSampleThreads>(keep, s_scan, tot_keep);
-    if (t < n) {
-      s_kc[t] = (uint16_t)c;
-      if (keep) s_eff[c] = w;
-    }
+    if (t < kBatchWords) s_kc[t] = (uint16_t)(c < kBatchWords ? c : kBatchWords);
+    if (keep && c < kBatchWords) s_eff[c] = w;
+    if (keep && c == kBatchWords - 1) s_cut_draws = p + 1;
     inv_base += tot_inv;
     keep_base += tot_keep;
   }
-  if (threadIdx.x == 0) s_kc[n] = (uint16_t)keep_base;
   __syncthreads();
+  const int kept = keep_base < kBatchWords ? keep_base : kBatchWords;
 
-  const uint32_t ndraw = a.sample_on ? (uint32_t)inv_base : 0u;
-  const int ns = (int)(s1 - s0);
+  const uint64_t ndraw =
+      a.sample_on ? (s_cut_draws >= 0 ? (uint64_t)s_cut_draws : (uint64_t)inv_base) : 0ull;
   const float alpha = WRITE ? a.job_alpha[jg] : 0.f;
   const int64_t out_base = WRITE ? a.job_exoff[j] : 0;
   const uint32_t cum_last = a.cum[a.V - 1];
@@ -80,30 +103,45 @@ __global__ __launch_bounds__(kSampleThreads) void k_job_sample(SampleArgs a) {
     const int q = q0 + threadIdx.x;
     int e0 = 0, e1 = 0;
     if (q < ns) {
-      e0 = s_kc[sent_start(a, s0 + q) - tb];
-      e1 = s_kc[sent_start(a, s0 + q + 1) - tb];
+      // kept-before count at a sentence boundary (the job end: all kept words)
+      const int64_t b0 = sent_start(a, s0 + q) - tb, b1 = sent_start(a, s0 + q + 1) - tb;
+      e0 = b0 >= n ? kept : s_kc[b0];
+      e1 = b1 >= n ? kept : s_kc[b1];
     }
     const int L = e1 - e0;
     const int nex = L >= 2 ? 2 * (L - 1) : 0;  // window 1: (i,i-1),(i,i+1) in range
     int tot;
     const int eb = ex_base + block_excl_scan<kSampleThreads>(nex, s_scan, tot);
-    if (WRITE && nex) {
+    // example k of a sentence of L kept words, in gensim's loop order:
+    // k = 0 -> (0, 1); k >= 1 -> i = (k+1)/2, j = i-1 (k odd) or i+1 (k even)
+    auto write_rec = [&](int e, int i, int jj) {
+      int32_t* r = a.rec + (out_base + e) * a.rec_stride;
+      const int32_t center = s_eff[i];
+      r[0] = center;
+      r[1] = s_eff[jj];
+      r[2] = __float_as_int(alpha);
+      uint64_t nr = lcg_jump_big(seed, ndraw + (uint64_t)a.K * (uint64_t)e, a.jump);
+      for (int d = 0; d < a.K; ++d) {
+        const int32_t t = draw_negative(nr, a.cum, a.bkt, a.V, cum_last);
+        r[3 + d] = (t == center) ? -1 : t;
+      }
+    };
+    if (WRITE && ns == 1) {
+      // one sentence (long ones always are; it starts at kept word 0): its
+      // examples spread over the whole block (tot = its example count)
+      for (int k = threadIdx.x; k < tot; k += kSampleThreads) {
+        const int i = (k + 1) >> 1;
+        const int jj = k == 0 ? 1 : ((k & 1) ? i - 1 : i + 1);
+        write_rec(k, i, jj);
+      }
+    } else if (WRITE && nex) {
       int e = eb;
       for (int i = e0; i < e1; ++i) {
 #pragma unroll
         for (int dj = -1; dj <= 1; dj += 2) {
           const int jj = i + dj;
           if (jj < e0 || jj >= e1) continue;
-          int32_t* r = a.rec + (out_base + e) * a.rec_stride;
-          const int32_t center = s_eff[i];
-          r[0] = center;
-          r[1] = s_eff[jj];
-          r[2] = __float_as_int(alpha);
-          uint64_t nr = lcg_jump(seed, ndraw + (uint32_t)a.K * (uint32_t)e, a.jump);
-          for (int d = 0; d < a.K; ++d) {
-            const int32_t t = draw_negative(nr, a.cum, a.bkt, a.V, cum_last);
-            r[3 + d] = (t == center) ? -1 : t;
-          }
+          write_rec(e, i, jj);
           ++e;
         }
       }
@@ -112,8 +150,10 @@ __global__ __launch_bounds__(kSampleThreads) void k_job_sample(SampleArgs a) {
   }
   if (!WRITE && threadIdx.x == 0) {
     a.job_nex[j] = ex_base;
-    atomicAdd(a.counters + 0, (unsigned long long)keep_base);  // effective words
-    atomicAdd(a.counters + 2, (unsigned long long)n);          // raw words
+    atomicAdd(a.counters + 0, (unsigned long long)kept);   // effective words
+    atomicAdd(a.counters + 2, (unsigned long long)n_raw);  // raw words
+    const unsigned long long f = (s_bad ? kFaultTokenRange : 0ull) | (bad_job ? kFaultJobSize : 0ull);
+    if (f) atomicOr(a.counters + 3, f);
   }
 }
 
@@ -310,6 +350,136 @@ hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
   if (rows <= 0 || copies <= 1) return hipSuccess;
   hipLaunchKernelGGL(k_fold_stripes, dim3(rows, 2), dim3(128), 0, st, syn0, syn1, stripe, rows,
                      copies, ld, nvec);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// replica merge (g2v_average / g2v_average_local): one wave per row, lane l
+// owns float4 columns l, l+64; HBM-bound streaming (rows are 128-B aligned)
+// ---------------------------------------------------------------------------
+// t <- t - old (the replica's change since the last merge, summed over ranks
+// by the all-reduce that follows), cnt[row] = 1 if the row changed
+__global__ __launch_bounds__(256) void k_merge_delta(float* __restrict__ t,
+                                                     const float* __restrict__ old,
+                                                     float* __restrict__ cnt, int64_t V,
+                                                     int64_t ld, int nvec) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= V) return;
+  float4* tr = reinterpret_cast<float4*>(t + r * ld);
+  const float4* orw = reinterpret_cast<const float4*>(old + r * ld);
+  int nz = 0;
+  for (int c = lane; c < nvec; c += 64) {
+    const float4 x = tr[c], o = orw[c];
+    const float4 d = make_float4(x.x - o.x, x.y - o.y, x.z - o.z, x.w - o.w);
+    nz |= (d.x != 0.f) | (d.y != 0.f) | (d.z != 0.f) | (d.w != 0.f);
+    tr[c] = d;
+  }
+  const int any = __any(nz);
+  if (lane == 0) cnt[r] = any ? 1.f : 0.f;
+}
+
+// after the all-reduce: touch (rule 0) t holds sum_r d_r, cnt the number of
+// replicas that changed the row: new = old + t / max(cnt, 1); mean (rule 1)
+// t holds sum_r t_r: new = t * inv_n.  Both: old = t = new.
+__global__ __launch_bounds__(256) void k_merge_apply(float* __restrict__ t, float* __restrict__ old,
+                                                     const float* __restrict__ cnt, int64_t V,
+                                                     int64_t ld, int nvec, int rule, float inv_n) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= V) return;
+  float4* tr = reinterpret_cast<float4*>(t + r * ld);
+  float4* orw = reinterpret_cast<float4*>(old + r * ld);
+  const float k = rule == 0 ? fmaxf(cnt[r], 1.f) : 1.f;
+  for (int c = lane; c < nvec; c += 64) {
+    const float4 x = tr[c];
+    float4 nv;
+    if (rule == 0) {
+      const float4 o = orw[c];
+      nv = make_float4(o.x + x.x / k, o.y + x.y / k, o.z + x.z / k, o.w + x.w / k);
+    } else {
+      nv = make_float4(x.x * inv_n, x.y * inv_n, x.z * inv_n, x.w * inv_n);
+    }
+    tr[c] = nv;
+    orw[c] = nv;
+  }
+}
+
+// n replicas on one device: the whole merge in one pass (deltas summed in
+// replica order)
+__global__ __launch_bounds__(256) void k_merge_local(LocalMergeArgs a, int n, int64_t V,
+                                                     int64_t ld, int nvec, int rule) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= V) return;
+  const int64_t base = r * ld;
+  int k = 0;
+  if (rule == 0) {
+    for (int i = 0; i < n; ++i) {
+      const float4* tr = reinterpret_cast<const float4*>(a.t[i] + base);
+      const float4* orw = reinterpret_cast<const float4*>(a.old[i] + base);
+      int nz = 0;
+      for (int c = lane; c < nvec; c += 64) {
+        const float4 x = tr[c], o = orw[c];
+        nz |= (x.x - o.x != 0.f) | (x.y - o.y != 0.f) | (x.z - o.z != 0.f) | (x.w - o.w != 0.f);
+      }
+      k += __any(nz) ? 1 : 0;
+    }
+  }
+  const float kf = k > 1 ? (float)k : 1.f;
+  const float inv_n = 1.f / (float)n;
+  for (int c = lane; c < nvec; c += 64) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < n; ++i) {
+      const float4 x = reinterpret_cast<const float4*>(a.t[i] + base)[c];
+      if (rule == 0) {
+        const float4 o = reinterpret_cast<const float4*>(a.old[i] + base)[c];
+        s.x += x.x - o.x;
+        s.y += x.y - o.y;
+        s.z += x.z - o.z;
+        s.w += x.w - o.w;
+      } else {
+        s.x += x.x;
+        s.y += x.y;
+        s.z += x.z;
+        s.w += x.w;
+      }
+    }
+    float4 nv;
+    if (rule == 0) {
+      const float4 o = reinterpret_cast<const float4*>(a.old[0] + base)[c];
+      nv = make_float4(o.x + s.x / kf, o.y + s.y / kf, o.z + s.z / kf, o.w + s.w / kf);
+    } else {
+      nv = make_float4(s.x * inv_n, s.y * inv_n, s.z * inv_n, s.w * inv_n);
+    }
+    for (int i = 0; i < n; ++i) {
+      reinterpret_cast<float4*>(a.t[i] + base)[c] = nv;
+      reinterpret_cast<float4*>(a.old[i] + base)[c] = nv;
+    }
+  }
+}
+
+hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V, int64_t ld,
+                              int nvec, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_delta, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, old, cnt,
+                     V, ld, nvec);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V, int64_t ld,
+                              int nvec, int rule, float inv_n, hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_apply, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, old, cnt,
+                     V, ld, nvec, rule, inv_n);
+  return hipGetLastError();
+}
+
+hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
+                              int rule, hipStream_t st) {
+  if (V <= 0 || n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_merge_local, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, a, n, V, ld,
+                     nvec, rule);
   return hipGetLastError();
 }
 

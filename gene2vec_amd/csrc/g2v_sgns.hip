@@ -57,6 +57,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
   bool eon[NE];
 #pragma unroll
   for (int i = 0; i < NE; ++i) eon[i] = (lane + 64 * i) < D;
+  // compute_loss: SEQUENTIAL continues gensim's float32 running sum in its
+  // order; the parallel modes add each wave's per-chunk float partial in double
+  const bool closs = a.compute_loss != 0;
+  float lsum = (closs && MODE == kModeSequential) ? *a.loss_f32 : 0.f;
 
   for (int64_t c = gw; c * kChunk < E; c += nw) {
     const int64_t e_end = (c * kChunk + kChunk < E) ? c * kChunk + kChunk : E;
@@ -136,6 +140,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
         if (f <= -(float)kMaxExp || f >= (float)kMaxExp) continue;
         const int idx = (int)((f + (float)kMaxExp) * (float)kLutScale);
         const float g = ((d == 0 ? 1.0f : 0.0f) - s_lut[idx]) * alpha;
+        if (closs) {
+          // [ext] f_dot = (f_dot if d == 0 else -f_dot); loss -= LOG_TABLE[idx(f_dot)]
+          const float fl = d == 0 ? f : -f;
+          lsum = lsum - a.log_table[(int)((fl + (float)kMaxExp) * (float)kLutScale)];
+        }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           work[v].x = __fmaf_rn(g, rw[d][v].x, work[v].x);
@@ -217,7 +226,12 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns(SgnsArgs a) {
         }
       }
     }
+    if (closs && MODE != kModeSequential) {
+      if (lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);
+      lsum = 0.f;
+    }
   }
+  if (closs && MODE == kModeSequential && lane == 0) *a.loss_f32 = lsum;
 }
 
 

@@ -108,14 +108,21 @@ __device__ __forceinline__ void upd(float* p, float v) {
   else if (WR == 1) *p = v;
 }
 
-template <int K, int NV, int WR = 0>
+// LOSS ([ext] compute_loss): each wave keeps a float32 partial of the
+// -log(sigmoid(+-f)) LOG_TABLE terms over its chunk and adds it to a double
+// accumulator once per chunk; LOSS = false compiles the tally out.
+template <int K, int NV, int WR = 0, bool LOSS = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
   __shared__ float s_lut[kExpTableSize];
+  __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
   __shared__ float s_wk[W][256 * NV];
-  for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) s_lut[i] = a.exp_table[i];
+  for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
+    s_lut[i] = a.exp_table[i];
+    if (LOSS) s_log[i] = a.log_table[i];
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -140,6 +147,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   for (int64_t c = gw; c * kChunk < E; c += nw) {
     const int64_t e_beg = c * kChunk;
     const int64_t e_end = (e_beg + kChunk < E) ? e_beg + kChunk : E;
+    float lsum = 0.f;
     ExRegs<K, NV> x;
     load_example<K, NV>(x, a, e_beg, r0, r1, rowb, lane, on);
     for (int64_t e = e_beg; e < e_end; ++e) {
@@ -185,6 +193,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         if (f <= -(float)kMaxExp || f >= (float)kMaxExp) continue;
         const int idx = (int)((f + (float)kMaxExp) * (float)kLutScale);
         const float gg = ((d == 0 ? 1.0f : 0.0f) - s_lut[idx]) * x.alpha;
+        if (LOSS) {
+          const float fl = d == 0 ? f : -f;
+          lsum = lsum - s_log[(int)((fl + (float)kMaxExp) * (float)kLutScale)];
+        }
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           work[v].x = __fmaf_rn(gg, x.rw[d][v].x, work[v].x);
@@ -283,6 +295,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
       __builtin_amdgcn_wave_barrier();
     }
+    if (LOSS && lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);
   }
 }
 
@@ -314,6 +327,15 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
     return hipGetLastError();
   }
 #endif
+  if (a.compute_loss) {
+    if (nv == 1)
+      hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true>), dim3(grid), dim3(kSgnsThreads), 0, st,
+                         a);
+    else
+      hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 2, 0, true>), dim3(grid), dim3(kSgnsThreads), 0, st,
+                         a);
+    return hipGetLastError();
+  }
   if (nv == 1)
     hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
   else

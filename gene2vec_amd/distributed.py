@@ -1,14 +1,19 @@
-"""Data-parallel SGNS across GPUs: one process per GPU, torch.distributed.
+"""Data-parallel SGNS across GPUs: one process per GPU.
 
 The reference has no distribution (gensim Hogwild threads in one process,
 src/gene2vec.py:59).  Pairs are independent SGNS examples, so the corpus is
 sharded by contiguous pair ranges; every rank keeps a full replica of
-syn0/syn1neg (torch-owned device tensors bound into libg2v) and trains its
-shard; every ``avg_every_jobs`` gensim jobs the replicas are averaged with one
-all-reduce per table (backend "nccl" = RCCL over xGMI on MI355X; "gloo" on
-CPU for tests).  The vocabulary is global: counts are summed and first
-occurrences reduced with MIN over global token positions, so every rank
-builds the identical index order and cum_table.
+syn0/syn1neg and trains its shard; every ``avg_every_jobs`` gensim jobs the
+replicas are merged.  The production merge runs inside libg2v
+(``g2v_comm_init`` / ``g2v_average``: fused HIP delta/apply kernels around one
+grouped ncclAllReduce over xGMI on the context's stream); torch.distributed
+only bootstraps it (the RCCL unique id, the vocabulary, scalar agreements).
+The ``torch`` merge backend (row-wise merge of torch-bound tables with
+torch.distributed collectives) remains for gloo: CPU tests and rehearsals
+with several ranks sharing one GPU, which RCCL refuses ("Duplicate GPU").
+The vocabulary is global: counts are summed and first occurrences reduced
+with MIN over global token positions, so every rank builds the identical
+index order and cum_table.
 """
 from __future__ import annotations
 
@@ -100,36 +105,101 @@ def touch_merge_(tensors, olds, beta=1.0, group=None):
         t.copy_(old)
 
 
+def world_size(group=None):
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(group)
+    return 1
+
+
+def allreduce_max_int(v, group=None):
+    """max over ranks of a Python int (a CPU tensor for gloo, a device tensor
+    for nccl); the int itself without a process group"""
+    import torch
+    import torch.distributed as dist
+    if world_size(group) == 1:
+        return int(v)
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def allreduce_sum_float(v, group=None):
+    import torch
+    import torch.distributed as dist
+    if world_size(group) == 1:
+        return float(v)
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([float(v)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, group=group)
+    return float(t.item())
+
+
+MERGE_RULES = {"touch": 0, "mean": 1}  # == G2V_MERGE_TOUCH / G2V_MERGE_MEAN
+
+
 class ReplicaTrainer:
     """Drives one rank: trains job windows on an engine-like object and
     merges the replicas between windows.
 
-    engine: has ``train(job_sent, alpha, seed, mode, timing=...)``.
-    tables: the torch tensors bound into the engine (merged in place).
-    merge:  "touch" (row-wise, default) or "mean" (plain model averaging).
+    engine:  has ``train(job_sent, alpha, seed, mode, timing=..., compute_loss=...)``
+             and, for backend "rccl", ``average(rule)`` (libg2v's g2v_average
+             after g2v_comm_init).
+    tables:  backend "torch" only: the torch tensors bound into the engine.
+    merge:   "touch" (row-wise, default) or "mean" (plain model averaging).
+    backend: "rccl" (merge inside libg2v) or "torch" (torch.distributed).
+
+    Every rank runs the same number of windows, the maximum over ranks (a
+    rank out of jobs still joins each merge), so shards whose job counts
+    differ cannot leave a rank waiting in a collective.  One process: no
+    merges at all.
     """
 
-    def __init__(self, engine, tables, avg_every_jobs, mode=0, merge="touch", beta=1.0):
+    def __init__(self, engine, tables=(), avg_every_jobs=1024, mode=0, merge="touch", beta=1.0,
+                 backend="torch", group=None):
+        if backend not in ("torch", "rccl"):
+            raise ValueError(backend)
         self.engine = engine
         self.tables = list(tables)
         self.avg_every_jobs = max(1, int(avg_every_jobs))
         self.mode = mode
         self.merge = merge
         self.beta = beta
-        self.olds = [t.clone() for t in self.tables] if merge == "touch" else None
+        self.backend = backend
+        self.group = group
+        self.olds = ([t.clone() for t in self.tables]
+                     if merge == "touch" and backend == "torch" else None)
         self.averages = 0
 
-    def train_epoch(self, job_sent, alphas, seeds, timing=False):
+    def train_epoch(self, job_sent, alphas, seeds, timing=False, compute_loss=False):
         n_jobs = len(job_sent) - 1
-        for j0 in range(0, n_jobs, self.avg_every_jobs):
-            j1 = min(n_jobs, j0 + self.avg_every_jobs)
-            self.engine.train(job_sent[j0:j1 + 1], alphas[j0:j1], seeds[j0:j1], self.mode,
-                              timing=timing)
-            self.sync_replicas()
+        every = self.avg_every_jobs
+        world = world_size(self.group)
+        n_win = (n_jobs + every - 1) // every
+        if world > 1:
+            n_win = allreduce_max_int(n_win, self.group)
+        kw = {"timing": timing}
+        if compute_loss:
+            kw["compute_loss"] = True
+        for w in range(n_win):
+            j0 = w * every
+            j1 = min(n_jobs, j0 + every)
+            if j0 < n_jobs:
+                self.engine.train(job_sent[j0:j1 + 1], alphas[j0:j1], seeds[j0:j1], self.mode,
+                                  **kw)
+            if world > 1:
+                self.sync_replicas()
 
     def sync_replicas(self):
-        if self.merge == "touch":
-            touch_merge_(self.tables, self.olds, self.beta)
+        if self.backend == "rccl":
+            self.engine.average(MERGE_RULES[self.merge])
+        elif self.merge == "touch":
+            touch_merge_(self.tables, self.olds, self.beta, self.group)
         else:
-            average_(self.tables)
+            average_(self.tables, self.group)
         self.averages += 1

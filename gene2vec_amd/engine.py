@@ -112,6 +112,11 @@ class SGNSEngine:
     def set_option(self, key, value):
         N.check(self._lib.g2v_set_option(self._h, key, int(value)))
 
+    def get_option(self, key):
+        v = C.c_int64()
+        N.check(self._lib.g2v_get_option(self._h, key, C.byref(v)))
+        return v.value
+
     def set_stream(self, stream_handle):
         N.check(self._lib.g2v_set_stream(self._h, C.c_void_p(stream_handle or 0)))
 
@@ -174,21 +179,25 @@ class SGNSEngine:
         self.n_sent = n_sent
 
     # -- training ----------------------------------------------------------------
-    def train(self, job_sent, job_alpha, job_seed, mode=N.MODE_HOGWILD, timing=False):
+    def train(self, job_sent, job_alpha, job_seed, mode=N.MODE_HOGWILD, timing=False,
+              compute_loss=False):
         job_sent = np.ascontiguousarray(job_sent, dtype=np.int64)
         job_alpha = np.ascontiguousarray(job_alpha, dtype=np.float32)
         job_seed = np.ascontiguousarray(job_seed, dtype=np.uint64)
         n = len(job_sent) - 1
         assert len(job_alpha) == n and len(job_seed) == n
-        flags = mode | (N.FLAG_TIMING if timing else 0)
+        flags = (mode | (N.FLAG_TIMING if timing else 0)
+                 | (N.FLAG_COMPUTE_LOSS if compute_loss else 0))
         N.check(self._lib.g2v_train(self._h, N.ptr(job_sent), N.ptr(job_alpha), N.ptr(job_seed),
                                     n, flags))
 
-    def step_explicit(self, center, inp, negs, alpha, mode=N.MODE_SEQUENTIAL, timing=False):
+    def step_explicit(self, center, inp, negs, alpha, mode=N.MODE_SEQUENTIAL, timing=False,
+                      compute_loss=False):
         center = np.ascontiguousarray(center, dtype=np.int32)
         inp = np.ascontiguousarray(inp, dtype=np.int32)
         negs = np.ascontiguousarray(negs, dtype=np.int32).reshape(len(center), self.K)
-        flags = mode | (N.FLAG_TIMING if timing else 0)
+        flags = (mode | (N.FLAG_TIMING if timing else 0)
+                 | (N.FLAG_COMPUTE_LOSS if compute_loss else 0))
         N.check(self._lib.g2v_sgns_step_explicit(self._h, N.ptr(center), N.ptr(inp), N.ptr(negs),
                                                  len(center), C.c_float(alpha), flags))
 
@@ -203,6 +212,32 @@ class SGNSEngine:
         N.check(self._lib.g2v_debug_sample(self._h, N.ptr(job_sent), N.ptr(job_seed), n,
                                            N.ptr(out), len(out), C.byref(cnt)))
         return out[:cnt.value]
+
+    def reset_loss(self):
+        N.check(self._lib.g2v_reset_loss(self._h))
+
+    # -- replica averaging (multi-GPU) -----------------------------
+    @staticmethod
+    def comm_unique_id():
+        """128-byte RCCL unique id (rank 0 draws it, every rank receives it)."""
+        buf = (C.c_char * N.UNIQUE_ID_BYTES)()
+        N.check(N.lib().g2v_comm_unique_id(buf, N.UNIQUE_ID_BYTES))
+        return bytes(buf)
+
+    def comm_init(self, unique_id, nranks, rank):
+        buf = (C.c_char * N.UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
+        N.check(self._lib.g2v_comm_init(self._h, buf, nranks, rank))
+
+    def average(self, rule=N.MERGE_TOUCH):
+        N.check(self._lib.g2v_average(self._h, rule))
+
+    def merge_snapshot(self):
+        N.check(self._lib.g2v_merge_snapshot(self._h))
+
+    @staticmethod
+    def average_local(engines, rule=N.MERGE_TOUCH):
+        arr = (C.c_void_p * len(engines))(*[e._h.value for e in engines])
+        N.check(N.lib().g2v_average_local(arr, len(engines), rule))
 
     def sync(self):
         N.check(self._lib.g2v_sync(self._h))

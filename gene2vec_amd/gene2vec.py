@@ -24,7 +24,6 @@ import logging
 import os
 import random
 import time
-import zlib
 
 import numpy as np
 
@@ -53,10 +52,11 @@ def read_gene_pairs(source_dir, ending_pattern, rng=random):
 
 
 def _hashfxn(name):
+    from .word2vec import crc32_hash
     if name == "python":
         return hash
     if name == "crc32":
-        return lambda s: zlib.crc32(s.encode("utf-8"))
+        return crc32_hash
     raise ValueError(name)
 
 
@@ -227,7 +227,7 @@ def main(argv=None):
         outputs = []
         kw = dict(size=dimension, window=args.window, min_count=1, workers=args.workers, iter=1,
                   sg=1, negative=args.negative, sample=args.sample, hashfxn=hashfxn,
-                  device=args.device, mode=args.mode)
+                  device=args.device, mode=args.mode, data_parallel=world > 1)
         import gene2vec_amd.word2vec as W
         W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
         for current_iter in range(1, args.iters + 1):
@@ -265,6 +265,7 @@ def main(argv=None):
                 prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
                 with ph("load"):
                     model = Word2Vec.load(prev, device=args.device)
+                    model.data_parallel = world > 1
                 if corpus is None:
                     with ph("train"):
                         model.train(gene_pairs, total_examples=model.corpus_count,

@@ -23,6 +23,7 @@ import math
 import os
 import time
 import zipfile
+import zlib
 
 import numpy as np
 
@@ -295,6 +296,22 @@ def _load_npz(fname):
 DP_MERGE_EVERY_JOBS = 1024
 
 
+def crc32_hash(s):
+    """deterministic seeded_vector hash (the CLI's --hash crc32)"""
+    return zlib.crc32(s.encode("utf-8"))
+
+
+# hashfxn <-> name in the checkpoint (gensim pickles the function itself)
+_HASH_NAMES = {"python": hash, "crc32": crc32_hash}
+
+
+def _hash_name(fn):
+    for k, v in _HASH_NAMES.items():
+        if fn is v:
+            return k
+    return "custom"
+
+
 class Word2Vec:
     """Skip-gram negative-sampling Word2Vec trained on an MI355X.
 
@@ -303,13 +320,18 @@ class Word2Vec:
     is accepted for compatibility (the GPU kernel replaces the thread pool).
     Extra keyword ``device`` picks the GPU; ``mode`` = "hogwild" (default,
     all SGNS updates as memory-side atomics) or "sequential" (one wave,
-    gensim workers=1 order, for parity checks)."""
+    gensim workers=1 order, for parity checks); ``data_parallel`` = True
+    shards the corpus over an initialised torch.distributed group and merges
+    the replicas (opt-in: the gene2vec CLI sets it under torchrun; a model
+    trained inside some unrelated process group stays single-GPU).
+    ``compute_loss`` follows gensim 3.4: the running loss of the latest
+    train() call, ``get_latest_training_loss()``."""
 
     def __init__(self, sentences=None, size=100, alpha=0.025, window=5, min_count=5,
                  max_vocab_size=None, sample=1e-3, seed=1, workers=3, min_alpha=0.0001,
                  sg=0, hs=0, negative=5, cbow_mean=1, hashfxn=hash, iter=5, null_word=0,
                  trim_rule=None, sorted_vocab=1, batch_words=N.BATCH_WORDS, compute_loss=False,
-                 callbacks=(), ns_exponent=0.75, device=0, mode="hogwild"):
+                 callbacks=(), ns_exponent=0.75, device=0, mode="hogwild", data_parallel=False):
         if sg != 1:
             raise NotImplementedError("only skip-gram (sg=1) is implemented (src/gene2vec.py:60)")
         if hs:
@@ -345,6 +367,7 @@ class Word2Vec:
         self.callbacks = callbacks
         self.device = device
         self.mode = mode
+        self.data_parallel = data_parallel
         self.merge_every_jobs = DP_MERGE_EVERY_JOBS
         self.random = np.random.RandomState(seed)
         self.corpus_count = 0
@@ -363,7 +386,8 @@ class Word2Vec:
         if sentences is not None:
             self.build_vocab(sentences)
             self.train(sentences, total_examples=self.corpus_count, epochs=self.iter,
-                       start_alpha=self.alpha, end_alpha=self.min_alpha)
+                       start_alpha=self.alpha, end_alpha=self.min_alpha,
+                       compute_loss=compute_loss)
 
     # -- vocabulary ----------------------------------------------------------------
     def build_vocab(self, sentences, update=False, progress_per=10000, keep_raw_vocab=False,
@@ -411,9 +435,11 @@ class Word2Vec:
         self._replica = None
         self._dev_dirty = False
 
-    @staticmethod
-    def _dp_world():
-        """(rank, world) of an initialised torch.distributed group, else (0, 1)."""
+    def _dp_world(self):
+        """(rank, world) of the initialised torch.distributed group when this
+        model trains data-parallel (opt-in), else (0, 1)."""
+        if not getattr(self, "data_parallel", False):
+            return 0, 1
         try:
             import torch.distributed as dist
         except ImportError:  # pragma: no cover
@@ -424,13 +450,23 @@ class Word2Vec:
 
     def _bind_replica(self, eng):
         """Data-parallel replica (no reference equivalent: gensim is one process,
-        src/gene2vec.py:59): both tables in one torch-owned [2][V][ld] device
-        buffer bound into the engine, rank 0's values broadcast (Python's hash()
-        seeds the init differently in every process), and one ReplicaTrainer
-        merging the replicas row-wise every ``merge_every_jobs`` jobs over the
-        process group (RCCL over xGMI with backend "nccl")."""
+        src/gene2vec.py:59).  Backend "nccl": libg2v joins an RCCL communicator
+        (unique id broadcast over the process group), takes rank 0's tables
+        (Python's hash() seeds the init differently in every process) and
+        merges the replicas itself every ``merge_every_jobs`` jobs (fused HIP
+        kernels + ncclAllReduce over xGMI).  Backend "gloo" (ranks sharing one
+        GPU, which RCCL refuses): torch-owned tables merged by torch.distributed."""
         import torch
         import torch.distributed as dist
+        mode = N.MODE_SEQUENTIAL if self.mode == "sequential" else N.MODE_HOGWILD
+        rank, world = dist.get_rank(), dist.get_world_size()
+        if dist.get_backend() == "nccl":
+            box = [eng.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(box, src=0)
+            eng.comm_init(box[0], world, rank)
+            self._replica = Dd.ReplicaTrainer(eng, (), self.merge_every_jobs, mode,
+                                              backend="rccl")
+            return
         dev = torch.device("cuda", self.device)
         # engine launches, merges and collectives ordered on one non-default stream
         stream = torch.cuda.Stream(dev)
@@ -442,8 +478,8 @@ class Word2Vec:
         tables[1, :, :D] = torch.from_numpy(np.ascontiguousarray(self.syn1neg)).to(dev)
         dist.broadcast(tables, src=0)
         eng.bind_tables(tables[0].data_ptr(), tables[1].data_ptr(), eng.ld, keepalive=(tables,))
-        mode = N.MODE_SEQUENTIAL if self.mode == "sequential" else N.MODE_HOGWILD
-        self._replica = Dd.ReplicaTrainer(eng, (tables,), self.merge_every_jobs, mode)
+        self._replica = Dd.ReplicaTrainer(eng, (tables,), self.merge_every_jobs, mode,
+                                          backend="torch")
 
     def _ensure_engine(self):
         if self._engine is not None:
@@ -498,16 +534,23 @@ class Word2Vec:
             raise ValueError("You must specify either total_examples or total_words")
         tok, off = self._corpus_ids(sentences)
         return self.train_ids(tok, off, total_examples=total_examples, total_words=total_words,
-                              epochs=epochs, start_alpha=start_alpha, end_alpha=end_alpha)
+                              epochs=epochs, start_alpha=start_alpha, end_alpha=end_alpha,
+                              compute_loss=compute_loss)
 
     def train_ids(self, tokens, sent_off=None, sent_len=0, total_examples=None,
-                  total_words=None, epochs=1, start_alpha=None, end_alpha=None):
+                  total_words=None, epochs=1, start_alpha=None, end_alpha=None,
+                  compute_loss=False):
         """Fast path: pre-tokenised corpus (int32 vocabulary indices, -1 = OOV)
         as CSR sentence offsets or fixed-length sentences (pairs: sent_len=2)."""
         self.alpha = float(start_alpha or self.alpha)
         self.min_alpha = float(end_alpha or self.min_alpha)
         self.epochs = epochs
+        # [ext] BaseWordEmbeddingsModel.train: compute_loss is per call and the
+        # running loss restarts at 0.0 every train()
+        self.compute_loss = bool(compute_loss)
+        self.running_training_loss = 0.0
         eng = self._ensure_engine()
+        eng.reset_loss()
         rank, world = self._dp_world()
         if world > 1:
             # contiguous shard of the (shuffled) sentences per rank; alpha follows
@@ -559,10 +602,10 @@ class Word2Vec:
                 base = int(self.random.randint(0, 2 ** 31 - 1))
                 seeds = E.job_seeds(np.random.RandomState((base + 7919 * rank) % 2 ** 32),
                                     len(js) - 1)
-                self._replica.train_epoch(js, al, seeds)
+                self._replica.train_epoch(js, al, seeds, compute_loss=self.compute_loss)
             else:
                 seeds = E.job_seeds(self.random, len(js) - 1)
-                eng.train(js, al, seeds, mode)
+                eng.train(js, al, seeds, mode, compute_loss=self.compute_loss)
             st = eng.read_stats()
             stats.append(st)
             if len(al):
@@ -571,6 +614,10 @@ class Word2Vec:
                         cur_epoch + 1, st["raw_words"], st["effective_words"], st["examples"])
         self._dev_dirty = True
         self._sync_host()
+        if self.compute_loss and stats:
+            loss = stats[-1]["training_loss"]  # running since the reset above
+            # data parallel: the loss over every rank's shard
+            self.running_training_loss = Dd.allreduce_sum_float(loss) if world > 1 else loss
         elapsed = time.time() - t0
         self.total_train_time += elapsed
         self.train_count += 1
@@ -583,6 +630,11 @@ class Word2Vec:
         logger.info("training on %d raw words (%d effective words) took %.1fs, %.0f effective "
                     "words/s", raw, eff, elapsed, eff / max(elapsed, 1e-9))
         return eff, raw
+
+    def get_latest_training_loss(self):
+        """[ext] Word2Vec.get_latest_training_loss: the running loss of the
+        latest train() call with compute_loss=True (0.0 otherwise)."""
+        return self.running_training_loss
 
     # -- persistence --------------------------------------------------------------------------
     def save(self, fname):
@@ -597,6 +649,8 @@ class Word2Vec:
                 "iter": self.iter, "epochs": self.epochs, "batch_words": self.batch_words,
                 "corpus_count": self.corpus_count, "corpus_total_words": self.corpus_total_words,
                 "train_count": self.train_count, "mode": self.mode,
+                "hashfxn": _hash_name(self.hashfxn),
+                "running_training_loss": float(self.running_training_loss),
                 "min_alpha_yet_reached": self.min_alpha_yet_reached,
                 "rng_pos": int(st[2]), "rng_has_gauss": int(st[3]),
                 "rng_cached_gaussian": float(st[4])}
@@ -627,13 +681,17 @@ class Word2Vec:
                   "corpus_count", "corpus_total_words", "train_count", "mode",
                   "min_alpha_yet_reached"):
             setattr(m, k, meta[k])
-        m.hashfxn = hash
+        name = meta.get("hashfxn", "python")
+        if name not in _HASH_NAMES:
+            logger.warning("model was trained with a custom hashfxn; reloading with hash()")
+        m.hashfxn = _HASH_NAMES.get(name, hash)
         m.compute_loss = False
         m.callbacks = ()
         m.device = 0
+        m.data_parallel = False
         m.merge_every_jobs = DP_MERGE_EVERY_JOBS
         m.total_train_time = 0.0
-        m.running_training_loss = 0.0
+        m.running_training_loss = float(meta.get("running_training_loss", 0.0))
         m.random = np.random.RandomState()
         m.random.set_state(("MT19937", arrs["rng_keys"], meta["rng_pos"], meta["rng_has_gauss"],
                             meta["rng_cached_gaussian"]))

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define G2V_ABI_VERSION 1
+#define G2V_ABI_VERSION 2
 
 /* status codes */
 #define G2V_OK 0
@@ -44,6 +44,7 @@ extern "C" {
 #define G2V_ENOMEM (-3)     /* allocation failed */
 #define G2V_ESTATE (-4)     /* call order violated (e.g. train before vocab) */
 #define G2V_ERANGE (-5)     /* input exceeds a documented limit */
+#define G2V_ECOMM (-6)      /* RCCL error or RCCL unavailable */
 
 /* g2v_train / g2v_sgns_step_explicit modes */
 #define G2V_MODE_HOGWILD 0    /* production: many waves, lock-free (gensim workers=N) */
@@ -52,6 +53,10 @@ extern "C" {
                                  deltas summed (float atomics) */
 #define G2V_MODE_MASK 0x3u
 #define G2V_FLAG_TIMING 0x100u /* record HIP events around each SGNS kernel launch */
+/* [ext] train_batch_sg(..., compute_loss=True): tally -log(sigmoid(+-f)) from
+ * LOG_TABLE for every applied target into the running training loss (see
+ * g2v_stats.training_loss / g2v_reset_loss).  Off: the kernels pay nothing. */
+#define G2V_FLAG_COMPUTE_LOSS 0x200u
 
 /* g2v_set_corpus flags */
 #define G2V_CORPUS_DEVICE 0x1u /* tokens / sent_off are device pointers (borrowed) */
@@ -71,6 +76,13 @@ typedef struct g2v_stats {
     int64_t launches;         /* SGNS-kernel launches */
     double sgns_kernel_ms;    /* sum of SGNS-kernel durations (G2V_FLAG_TIMING), else 0 */
     double sample_kernel_ms;  /* sum of sampling-kernel durations (G2V_FLAG_TIMING), else 0 */
+    /* running training loss since the last g2v_reset_loss (NOT reset by
+     * g2v_read_stats; gensim's model.running_training_loss, reset by every
+     * train() call).  SEQUENTIAL launches continue one float32 running sum in
+     * gensim order (train_batch_sg's REAL_t accumulator, bit for bit);
+     * HOGWILD/MINIBATCH launches add per-wave float32 partial sums in double
+     * (gensim's own workers>1 tally is a racy read-modify-write of that float). */
+    double training_loss;
 } g2v_stats;
 
 /* ---- errors / version --------------------------------------------------- */
@@ -95,7 +107,8 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_CACHE_POLICY  0 default, 1 write-through stores (sc1), 2 sc1 loads and
  *                         stores [1]
  *   G2V_OPT_SEG_JOBS      gensim jobs per sampling/update segment [1024]
- *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = CUs x occupancy [0]
+ *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = the staleness-bounded
+ *                         default (g2v_get_option reads it) [0]
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
  *                         2 uncached (re-allocates, zero-filled) [0]
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
@@ -113,6 +126,10 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_STRIPE_ROWS 7
 #define G2V_OPT_STRIPE_COPIES 8
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
+/* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
+ * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest
+ * row takes more updates per example than C4's, see g2v_set_vocab). */
+int g2v_get_option(g2v_ctx *ctx, int key, int64_t *value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);
 
@@ -122,7 +139,8 @@ int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);
  * index order (sorted by descending count).  Both tables are built ON THE
  * DEVICE (sequential double accumulation, round-half-even) and are
  * bit-identical to gensim's; optional host copies are returned (synchronises
- * when either out pointer is non-NULL).  sample == 0 disables downsampling. */
+ * when either out pointer is non-NULL).  sample == 0 disables downsampling.
+ * Also sizes the default Hogwild grid from the hottest row's update share. */
 int g2v_set_vocab(g2v_ctx *ctx, const int64_t *counts, double sample, double ns_exponent,
                   uint32_t *cum_out, uint32_t *sample_int_out);
 
@@ -143,15 +161,23 @@ int g2v_get_weights(g2v_ctx *ctx, float *syn0, float *syn1neg);
  * vocabulary, skipped without drawing, as gensim's vlookup miss), sent_off[n_sent+1]
  * int64.  sent_off may be NULL when every sentence has length sent_len > 0
  * (gene pairs: sent_len = 2).  Replaces the list[list[str]] gensim receives at
- * src/gene2vec.py:70,87.  Without G2V_CORPUS_DEVICE the arrays are copied. */
+ * src/gene2vec.py:70,87.  Without G2V_CORPUS_DEVICE the arrays are copied and
+ * every id is checked to lie in [-1, V) (G2V_EINVAL otherwise).  A device
+ * corpus is checked by the sampler as it reads it: an id outside [-1, V) is
+ * skipped like an OOV token and latches a device fault that the next
+ * g2v_sync / g2v_read_stats reports as G2V_EINVAL. */
 int g2v_set_corpus(g2v_ctx *ctx, const int32_t *tokens, int64_t n_tokens, const int64_t *sent_off,
                    int64_t n_sent, int64_t sent_len, uint32_t flags);
 
 /* ---- training ---------------------------------------------------------------- */
-/* Greedy job packing of [ext] BaseAny2VecModel._job_producer: a sentence joins
- * the current job while raw words <= batch_words.  Writes job_sent[n_jobs+1]
- * (sentence index boundaries) when job_sent != NULL and cap >= n_jobs+1.
- * Host-only, no context.  Sentences longer than batch_words -> G2V_ERANGE. */
+/* Job packing of [ext] BaseAny2VecModel._job_producer: a sentence joins the
+ * current job while raw words <= batch_words, otherwise the current job is
+ * queued and the sentence starts the next one.  A sentence longer than
+ * batch_words therefore always trains as a job of its own, and when it is the
+ * FIRST sentence the producer first queues an EMPTY job (which still draws its
+ * two model.random seeds in train_batch_sg): job_sent = {0, 0, 1, ...}.
+ * Writes job_sent[n_jobs+1] (sentence index boundaries) when job_sent != NULL
+ * and cap >= n_jobs+1.  Host-only, no context. */
 int g2v_plan_jobs(const int64_t *sent_off, int64_t n_sent, int64_t sent_len, int64_t batch_words,
                   int64_t *job_sent, int64_t cap, int64_t *n_jobs_out);
 
@@ -161,16 +187,25 @@ int g2v_plan_jobs(const int64_t *sent_off, int64_t n_sent, int64_t sent_len, int
  * job_alpha[n_jobs] the per-job learning rate of [ext] _update_job_params (A.6),
  * job_seed[n_jobs] the per-job next_random = 2**24*randint(2**24)+randint(2**24)
  * drawn from model.random.  Downsampling, the 48-bit LCG, the cum_table bisect and
- * the window-1 example order reproduce gensim exactly; mode selects the
- * update order (G2V_MODE_HOGWILD | G2V_MODE_SEQUENTIAL) | G2V_FLAG_TIMING. */
+ * the window-1 example order reproduce gensim exactly, including train_batch_sg's
+ * truncation at MAX_SENTENCE_LEN = 10000 effective words (a job holding more
+ * raw words must be a single sentence, as g2v_plan_jobs makes it; tokens after
+ * the 10000th kept word draw nothing and train nothing).  mode selects the
+ * update order (G2V_MODE_HOGWILD | G2V_MODE_SEQUENTIAL) | G2V_FLAG_TIMING |
+ * G2V_FLAG_COMPUTE_LOSS. */
 int g2v_train(g2v_ctx *ctx, const int64_t *job_sent, const float *job_alpha,
               const uint64_t *job_seed, int64_t n_jobs, uint32_t flags);
 
 /* Deterministic step with explicit negatives: n examples (center[i] = gensim
  * word_index, input[i] = word2_index whose syn0 row is trained, negs[i*K..] with
- * -1 = skipped), one learning rate.  Modes SEQUENTIAL / HOGWILD / MINIBATCH. */
+ * -1 = skipped), one learning rate.  Modes SEQUENTIAL / HOGWILD / MINIBATCH,
+ * optionally | G2V_FLAG_COMPUTE_LOSS. */
 int g2v_sgns_step_explicit(g2v_ctx *ctx, const int32_t *center, const int32_t *input,
                            const int32_t *negs, int64_t n, float alpha, uint32_t flags);
+
+/* [ext] BaseWordEmbeddingsModel.train resets model.running_training_loss to 0.0
+ * at the start of every train() call; this is that reset. */
+int g2v_reset_loss(g2v_ctx *ctx);
 
 /* Debug/parity: the (center, input, negs[K]) records the device sampler
  * produces for jobs [0, n_jobs) (same arguments as g2v_train), written to
@@ -179,9 +214,43 @@ int g2v_debug_sample(g2v_ctx *ctx, const int64_t *job_sent, const uint64_t *job_
                      int64_t n_jobs, int32_t *rec_out, int64_t cap, int64_t *n_out);
 
 /* ---- sync / stats ------------------------------------------------------------ */
+/* Synchronises the context's stream; reports (and clears) a latched device
+ * fault of the sampler (corpus id outside [-1, V), or a multi-sentence job of
+ * more than 10000 raw words in a device corpus) as G2V_EINVAL. */
 int g2v_sync(g2v_ctx *ctx);
-/* Accumulated since the previous call (synchronises, then resets). */
+/* Accumulated since the previous call (synchronises, then resets; the running
+ * training_loss is only reset by g2v_reset_loss).  Reports a latched device
+ * fault like g2v_sync. */
 int g2v_read_stats(g2v_ctx *ctx, g2v_stats *out);
+
+/* ---- multi-GPU replica averaging (no reference equivalent:
+ * gensim is one process, src/gene2vec.py:59) ----------------------------------- */
+/* merge rules of g2v_average / g2v_average_local */
+#define G2V_MERGE_TOUCH 0 /* row-wise: new = old + sum_r(d_r) / k, d_r = replica r's change
+                             since the last merge, k = replicas whose row changed */
+#define G2V_MERGE_MEAN 1  /* plain model averaging: new = sum_r(t_r) / nranks */
+/* rank 0 draws an RCCL unique id (128 bytes, ncclGetUniqueId) to hand to every
+ * rank out of band (the Python driver broadcasts it over torch.distributed). */
+int g2v_comm_unique_id(void *id_out, int64_t id_bytes);
+/* Join the RCCL communicator of nranks processes (one GPU each, over xGMI),
+ * broadcast rank 0's tables to every rank (ncclBroadcast) and record them as
+ * the merge snapshot.  RCCL is loaded at run time (dlopen "librccl.so.1"):
+ * G2V_ECOMM when it is absent.  Collective: every rank must call it. */
+int g2v_comm_init(g2v_ctx *ctx, const void *rccl_unique_id, int nranks, int rank);
+/* Merge the replicas of every rank in place (collective: every rank calls it
+ * the same number of times): one fused HIP kernel forms the row deltas against
+ * the snapshot and the touched-row counts, one ncclAllReduce (grouped) sums
+ * them over xGMI on the context's stream, a second kernel applies the rule and
+ * refreshes the snapshot.  No communicator: no-op; a one-rank communicator
+ * runs the whole path (an identity on the values; callers skip it at N = 1). */
+int g2v_average(g2v_ctx *ctx, int merge_rule);
+/* Record the current tables as the merge snapshot (after replacing weights;
+ * g2v_comm_init and g2v_set_weights do it when a communicator exists). */
+int g2v_merge_snapshot(g2v_ctx *ctx);
+/* The same merge over n contexts of ONE process on ONE device (replicas
+ * trained by separate contexts, e.g. one per stream): no RCCL, one kernel.
+ * Every context needs a snapshot (g2v_merge_snapshot) and equal V, D, ld. */
+int g2v_average_local(g2v_ctx *const *ctxs, int n, int merge_rule);
 
 /* ---- text exporters ------------------------------------------------------------- */
 /* Row text of the two exporters, every float32 printed as numpy's

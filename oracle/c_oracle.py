@@ -30,7 +30,7 @@ def lib():
 
 
 def _p(a):
-    return a.ctypes.data_as(C.c_void_p)
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
 
 
 def make_cum_table(counts, power=0.75):
@@ -53,14 +53,43 @@ def exp_table():
     return out
 
 
+def log_table():
+    out = np.zeros(1000, dtype=np.float32)
+    lib().orc_log_table(_p(out))
+    return out
+
+
 def _u32_sample(sample_int):
     return np.minimum(np.asarray(sample_int, dtype=np.uint64), 0xFFFFFFFF).astype(np.uint32)
 
 
 def train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum, syn0,
-          syn1neg, lockf, K, nthreads=0):
+          syn1neg, lockf, K, nthreads=0, loss=None, ld=None):
     """In-place training of syn0/syn1neg ([V][D] float32 C-order).
-    nthreads == 0: sequential (workers=1 order); > 0: OpenMP Hogwild."""
+    nthreads == 0: sequential (workers=1 order); > 0: OpenMP Hogwild.
+    loss: None, or a float32 array of one element holding gensim's running
+    training loss (compute_loss=True), continued in place (sequential only).
+    ld: row stride in floats for the training copy (Hogwild: a multiple of 16
+    keeps each row on cache lines of its own, so threads updating neighbouring
+    hot rows do not falsely share lines); None = D, in place."""
+    V, D = syn0.shape
+    if ld is not None and ld != D:
+        assert ld >= D
+        p0 = np.zeros((V, ld), np.float32)
+        p1 = np.zeros((V, ld), np.float32)
+        p0[:, :D] = syn0
+        p1[:, :D] = syn1neg
+        st = _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum,
+                    p0, p1, lockf, K, nthreads, loss, ld, D)
+        syn0[:] = p0[:, :D]
+        syn1neg[:] = p1[:, :D]
+        return st
+    return _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum,
+                  syn0, syn1neg, lockf, K, nthreads, loss, D, D)
+
+
+def _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum, syn0,
+           syn1neg, lockf, K, nthreads, loss, ld, D):
     tok = np.ascontiguousarray(tok, dtype=np.int32)
     sent_off = np.ascontiguousarray(sent_off, dtype=np.int64)
     job_sent = np.ascontiguousarray(job_sent, dtype=np.int64)
@@ -71,16 +100,19 @@ def train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, c
     lockf = np.ascontiguousarray(lockf, dtype=np.float32)
     assert syn0.dtype == np.float32 and syn0.flags.c_contiguous
     assert syn1neg.dtype == np.float32 and syn1neg.flags.c_contiguous
-    V, D = syn0.shape
+    V = syn0.shape[0]
     stats = np.zeros(4, dtype=np.int64)
     n_jobs = len(job_sent) - 1
     args = [_p(tok), _p(sent_off), _p(job_sent), C.c_int64(n_jobs), _p(job_alpha), _p(job_seed),
             _p(si), C.c_int(int(bool(sample_on))), _p(cum), C.c_int32(V), _p(syn0), _p(syn1neg),
-            _p(lockf), C.c_int64(D), C.c_int32(D), C.c_int32(K)]
+            _p(lockf), C.c_int64(ld), C.c_int32(D), C.c_int32(K)]
     if nthreads and nthreads > 0:
+        assert loss is None, "the oracle tallies the loss in sequential order only"
         lib().orc_train_hogwild(*args, C.c_int(nthreads), _p(stats))
     else:
-        lib().orc_train_sequential(*args, _p(stats))
+        if loss is not None:
+            assert loss.dtype == np.float32 and loss.size == 1
+        lib().orc_train_sequential(*args, _p(stats), _p(loss))
     return dict(raw_words=int(stats[0]), effective_words=int(stats[1]), examples=int(stats[2]),
                 jobs=int(stats[3]))
 
@@ -103,7 +135,7 @@ def sample_records(tok, sent_off, job_sent, job_seed, sample_int, sample_on, cum
     return out[:n]
 
 
-def sgns_step_sequential(syn0, syn1neg, lockf, center, inp, negs, alpha):
+def sgns_step_sequential(syn0, syn1neg, lockf, center, inp, negs, alpha, loss=None):
     V, D = syn0.shape
     center = np.ascontiguousarray(center, dtype=np.int32)
     inp = np.ascontiguousarray(inp, dtype=np.int32)
@@ -111,7 +143,7 @@ def sgns_step_sequential(syn0, syn1neg, lockf, center, inp, negs, alpha):
     lockf = np.ascontiguousarray(lockf, dtype=np.float32)
     lib().orc_sgns_step_sequential(_p(syn0), _p(syn1neg), _p(lockf), C.c_int64(D), C.c_int32(D),
                                    C.c_int32(negs.shape[1]), _p(center), _p(inp), _p(negs),
-                                   C.c_int64(len(center)), C.c_float(alpha))
+                                   C.c_int64(len(center)), C.c_float(alpha), _p(loss))
 
 
 def count_records(tok, sent_off, job_sent, job_seed, sample_int, sample_on, cum, K):

@@ -7,6 +7,7 @@
  *   orc_make_cum_table   [ext] Word2VecVocab.make_cum_table      (A.3)
  *   orc_sample_int       [ext] Word2VecVocab.prepare_vocab        (A.2)
  *   orc_exp_table        [ext] word2vec_inner.pyx init()          (A.5)
+ *   orc_log_table        [ext] init(): LOG_TABLE[i] = <REAL_t>log(EXP_TABLE[i])
  *   orc_train_sequential [ext] train_batch_sg + fast_sentence_sg_neg, jobs in
  *                        order (= gensim with workers=1), driven the way
  *                        src/gene2vec.py:70,87 drives it
@@ -32,6 +33,7 @@
 #define LCG_MASK 281474976710655ULL
 
 static float g_exp_table[EXP_TABLE_SIZE];
+static float g_log_table[EXP_TABLE_SIZE];
 static int g_exp_ready = 0;
 
 void orc_exp_table(float *out) {
@@ -42,9 +44,16 @@ void orc_exp_table(float *out) {
     }
 }
 
+void orc_log_table(float *out) {
+    float e[EXP_TABLE_SIZE];
+    orc_exp_table(e);
+    for (int i = 0; i < EXP_TABLE_SIZE; i++) out[i] = (float)log((double)e[i]);
+}
+
 static void ensure_exp(void) {
     if (!g_exp_ready) {
         orc_exp_table(g_exp_table);
+        orc_log_table(g_log_table);
         g_exp_ready = 1;
     }
 }
@@ -107,10 +116,13 @@ static inline void saxpy(float g, const float *x, float *y, int D) {
 }
 
 /* [ext] fast_sentence_sg_neg; returns the advanced LCG state.  negs != NULL:
- * explicit negatives (-1 = skipped) replace the LCG/bisect draw. */
+ * explicit negatives (-1 = skipped) replace the LCG/bisect draw.  loss != NULL
+ * (compute_loss): *loss -= LOG_TABLE[int((+-f + 6) * 83)] per applied target,
+ * in float, in gensim's order. */
 static uint64_t sg_neg(int K, const uint32_t *cum, int32_t V, float *syn0, float *syn1neg,
                        int64_t ld, int D, int32_t word_index, int32_t word2_index, float alpha,
-                       float *work, uint64_t nr, const float *lockf, const int32_t *negs) {
+                       float *work, uint64_t nr, const float *lockf, const int32_t *negs,
+                       float *loss) {
     float *l1 = syn0 + (int64_t)word2_index * ld;
     memset(work, 0, sizeof(float) * D);
     for (int d = 0; d <= K; d++) {
@@ -133,6 +145,10 @@ static uint64_t sg_neg(int K, const uint32_t *cum, int32_t V, float *syn0, float
         float *row = syn1neg + (int64_t)t * ld;
         float f = dsdot(l1, row, D);
         if (f <= -MAX_EXP || f >= MAX_EXP) continue;
+        if (loss) {
+            const float fl = d == 0 ? f : -f;
+            *loss = *loss - g_log_table[(int)((fl + MAX_EXP) * LUT_SCALE)];
+        }
         f = g_exp_table[(int)((f + MAX_EXP) * LUT_SCALE)];
         float g = (label - f) * alpha;
         saxpy(g, row, work, D);
@@ -150,7 +166,7 @@ static int64_t train_job(const int32_t *tok, const int64_t *sent_off, int64_t s0
                          const uint32_t *cum, int32_t V, float *syn0, float *syn1neg,
                          const float *lockf, int64_t ld, int D, int K, float *work, int32_t *kept,
                          int32_t *sidx, int64_t *n_ex, int32_t *rec_out, int64_t rec_cap,
-                         int do_train) {
+                         int do_train, float *loss) {
     int32_t eff = 0, nsent = 0;
     sidx[0] = 0;
     for (int64_t s = s0; s < s1; s++) {
@@ -180,7 +196,7 @@ static int64_t train_job(const int32_t *tok, const int64_t *sent_off, int64_t s0
                 if (j == i) continue;
                 if (do_train) {
                     nr = sg_neg(K, cum, V, syn0, syn1neg, ld, D, kept[i], kept[j], alpha, work,
-                                nr, lockf, NULL);
+                                nr, lockf, NULL, loss);
                 } else if (rec_out && nex < rec_cap) {
                     int32_t *r = rec_out + nex * (K + 2);
                     r[0] = kept[i];
@@ -199,12 +215,13 @@ static int64_t train_job(const int32_t *tok, const int64_t *sent_off, int64_t s0
     return eff;
 }
 
-/* stats[0]=raw words, [1]=effective words, [2]=examples, [3]=jobs */
+/* stats[0]=raw words, [1]=effective words, [2]=examples, [3]=jobs.  loss:
+ * NULL, or gensim's float running training loss, continued in place */
 void orc_train_sequential(const int32_t *tok, const int64_t *sent_off, const int64_t *job_sent,
                           int64_t n_jobs, const float *job_alpha, const uint64_t *job_seed,
                           const uint32_t *sample_int, int sample_on, const uint32_t *cum,
                           int32_t V, float *syn0, float *syn1neg, const float *lockf, int64_t ld,
-                          int32_t D, int32_t K, int64_t *stats) {
+                          int32_t D, int32_t K, int64_t *stats, float *loss) {
     ensure_exp();
     float *work = (float *)malloc(sizeof(float) * D);
     int32_t *kept = (int32_t *)malloc(sizeof(int32_t) * MAX_SENTENCE_LEN);
@@ -214,7 +231,7 @@ void orc_train_sequential(const int32_t *tok, const int64_t *sent_off, const int
         int64_t nex = 0;
         eff += train_job(tok, sent_off, job_sent[j], job_sent[j + 1], job_alpha[j], job_seed[j],
                          sample_int, sample_on, cum, V, syn0, syn1neg, lockf, ld, D, K, work, kept,
-                         sidx, &nex, NULL, 0, 1);
+                         sidx, &nex, NULL, 0, 1, loss);
         ex += nex;
     }
     if (stats) {
@@ -248,7 +265,7 @@ void orc_train_hogwild(const int32_t *tok, const int64_t *sent_off, const int64_
             int64_t nex = 0;
             eff += train_job(tok, sent_off, job_sent[j], job_sent[j + 1], job_alpha[j],
                              job_seed[j], sample_int, sample_on, cum, V, syn0, syn1neg, lockf, ld,
-                             D, K, work, kept, sidx, &nex, NULL, 0, 1);
+                             D, K, work, kept, sidx, &nex, NULL, 0, 1, NULL);
             ex += nex;
         }
         free(work);
@@ -278,7 +295,7 @@ int64_t orc_sample_records(const int32_t *tok, const int64_t *sent_off, const in
         int64_t cap = rec_cap - total;
         train_job(tok, sent_off, job_sent[j], job_sent[j + 1], 0.0f, job_seed[j], sample_int,
                   sample_on, cum, V, NULL, NULL, NULL, 0, 0, K, NULL, kept, sidx, &nex,
-                  cap > 0 ? dst : NULL, cap, 0);
+                  cap > 0 ? dst : NULL, cap, 0, NULL);
         total += nex;
     }
     free(kept);
@@ -289,11 +306,11 @@ int64_t orc_sample_records(const int32_t *tok, const int64_t *sent_off, const in
 /* explicit-negative steps: mode 0 = sequential (gensim order) */
 void orc_sgns_step_sequential(float *syn0, float *syn1neg, const float *lockf, int64_t ld,
                               int32_t D, int32_t K, const int32_t *center, const int32_t *input,
-                              const int32_t *negs, int64_t n, float alpha) {
+                              const int32_t *negs, int64_t n, float alpha, float *loss) {
     ensure_exp();
     float *work = (float *)malloc(sizeof(float) * D);
     for (int64_t e = 0; e < n; e++)
         sg_neg(K, NULL, 0, syn0, syn1neg, ld, D, center[e], input[e], alpha, work, 0, lockf,
-               negs + e * K);
+               negs + e * K, loss);
     free(work);
 }

@@ -147,6 +147,11 @@ def exp_table():
     return (e / (e + np.float32(1))).astype(np.float32)
 
 
+def log_table():
+    """[ext] init(): LOG_TABLE[i] = <REAL_t>log(EXP_TABLE[i]) (C log of the float)."""
+    return np.log(exp_table().astype(np.float64)).astype(np.float32)
+
+
 def lcg_next(nr):
     return (nr * LCG_MUL + LCG_ADD) & LCG_MASK
 
@@ -258,11 +263,15 @@ def _axpy(g, x, y):
 
 
 def fast_sentence_sg_neg(K, cum, syn0, syn1neg, word_index, word2_index, alpha, nr,
-                         lockf, exp_tab, explicit_negs=None):
+                         lockf, exp_tab, explicit_negs=None, loss=None):
     """One directed example; returns the advanced LCG state.
 
     If ``explicit_negs`` (length K, -1 = skipped) is given, the LCG/bisect
-    draw is replaced by those targets (deterministic step API)."""
+    draw is replaced by those targets (deterministic step API).  ``loss``
+    (compute_loss=True): a one-element float32 array holding the running
+    training loss; every applied target subtracts
+    LOG_TABLE[int((f_dot + 6) * 83)], f_dot = +f for the positive and -f for a
+    negative, in float32 (train_batch_sg's REAL_t _running_training_loss)."""
     alpha = np.float32(alpha)
     l1 = syn0[word2_index]               # view; frozen until the end
     work = np.zeros(syn0.shape[1], dtype=np.float32)
@@ -287,10 +296,17 @@ def fast_sentence_sg_neg(K, cum, syn0, syn1neg, word_index, word2_index, alpha, 
             continue
         idx = int((f + np.float32(MAX_EXP)) * np.float32(LUT_SCALE))
         g = (label - exp_tab[idx]) * alpha
+        if loss is not None:
+            fl = f if d == 0 else -f
+            li = int((fl + np.float32(MAX_EXP)) * np.float32(LUT_SCALE))
+            loss[0] = np.float32(loss[0] - _LOG_TABLE[li])
         _axpy(g, row, work)
         _axpy(g, l1c, row)
     _axpy(lockf[word2_index], work, syn0[word2_index])
     return nr
+
+
+_LOG_TABLE = log_table()
 
 
 def downsample_job(tok_rows, sample_int, nr, sample_on):
@@ -339,10 +355,11 @@ def job_examples(kept_sents, window=1, reduced_windows=None):
 
 
 def train_job(tok_rows, alpha, seed, vocab_sample_int, sample_on, cum, syn0, syn1neg,
-              lockf, K, exp_tab, window=1):
+              lockf, K, exp_tab, window=1, loss=None):
     kept, nr, eff = downsample_job(tok_rows, vocab_sample_int, seed, sample_on)
     for c, j in job_examples(kept, window):
-        nr = fast_sentence_sg_neg(K, cum, syn0, syn1neg, c, j, alpha, nr, lockf, exp_tab)
+        nr = fast_sentence_sg_neg(K, cum, syn0, syn1neg, c, j, alpha, nr, lockf, exp_tab,
+                                  loss=loss)
     n_ex = len(job_examples(kept, window))
     return eff, n_ex
 
@@ -368,8 +385,9 @@ def sentences_to_ids(sentences, word2index):
 def train_epoch_sequential(id_sentences, vocab: Vocab, syn0, syn1neg, lockf, cum, K,
                            rs: np.random.RandomState, alpha=0.025, min_alpha=0.0001,
                            sample=1e-3, total_examples=None, cur_epoch=0, epochs=1,
-                           batch_words=10000, window=1):
-    """One epoch in gensim workers=1 order (jobs in order, seeds in order)."""
+                           batch_words=10000, window=1, loss=None):
+    """One epoch in gensim workers=1 order (jobs in order, seeds in order);
+    ``loss`` as in fast_sentence_sg_neg (compute_loss=True)."""
     if window != 1:
         raise NotImplementedError("oracle restates window=1 (src/gene2vec.py:62)")
     total_examples = total_examples or len(id_sentences)
@@ -382,7 +400,7 @@ def train_epoch_sequential(id_sentences, vocab: Vocab, syn0, syn1neg, lockf, cum
     eff_tot = ex_tot = 0
     for (s0, s1), a, sd in zip(jobs, alphas, seeds):
         eff, nex = train_job(id_sentences[s0:s1], a, sd, vocab.sample_int, sample_on,
-                             cum, syn0, syn1neg, lockf, K, exp_tab)
+                             cum, syn0, syn1neg, lockf, K, exp_tab, loss=loss)
         eff_tot += eff
         ex_tot += nex
     return dict(jobs=len(jobs), effective_words=eff_tot, examples=ex_tot,
@@ -392,13 +410,13 @@ def train_epoch_sequential(id_sentences, vocab: Vocab, syn0, syn1neg, lockf, cum
 # --------------------------------------------------------------------------
 # Deterministic step APIs (explicit negatives)
 # --------------------------------------------------------------------------
-def sgns_step_sequential(syn0, syn1neg, lockf, center, inp, negs, alpha):
+def sgns_step_sequential(syn0, syn1neg, lockf, center, inp, negs, alpha, loss=None):
     """Examples applied one after another (gensim semantics)."""
     exp_tab = exp_table()
     K = negs.shape[1]
     for e in range(len(center)):
         fast_sentence_sg_neg(K, None, syn0, syn1neg, int(center[e]), int(inp[e]),
-                             alpha, 0, lockf, exp_tab, explicit_negs=negs[e])
+                             alpha, 0, lockf, exp_tab, explicit_negs=negs[e], loss=loss)
 
 
 def sgns_step_minibatch(syn0, syn1neg, lockf, center, inp, negs, alpha):

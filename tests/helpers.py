@@ -91,3 +91,23 @@ def make_query(root, seed=0, studies=(("SRP1", 24), ("SRP2", 30), ("SRP3", 5)), 
     gc.insert(0, "gene_id", ids)
     gc.to_csv(os.path.join(root, "data/gene_counts.csv"), index=False)
     return root
+
+
+def long_sentence_corpus(seed=0):
+    """sentences over gensim's batch_words (40000 tokens first, so the job
+    producer queues an empty job; 12000; 10001) beside short and empty ones,
+    a downsampling-heavy word in the long head, OOV tokens.  Returns (tok,
+    sent_off, counts) in vocabulary index order."""
+    rng = np.random.RandomState(seed)
+    V = 20000
+    lengths = [40000, 3, 2, 12000, 0, 10001, 10000, 7]
+    tok = rng.randint(-1, V, size=sum(lengths)).astype(np.int32)
+    tok[:30000][rng.rand(30000) < 0.6] = 0           # a very frequent word: heavy downsampling
+    counts = np.bincount(tok[tok >= 0], minlength=V).astype(np.int64)
+    order = np.argsort(-counts, kind="stable")
+    order = order[counts[order] > 0]                  # words that occur
+    remap = np.full(V, -1, np.int32)
+    remap[order] = np.arange(len(order), dtype=np.int32)
+    tok = np.where(tok >= 0, remap[np.maximum(tok, 0)], -1).astype(np.int32)
+    off = np.cumsum([0] + lengths).astype(np.int64)
+    return tok, off, counts[order]

@@ -26,7 +26,7 @@ class FakeEngine:
     def __init__(self, tables, rank):
         self.tables, self.rank, self.calls = tables, rank, []
 
-    def train(self, js, al, sd, mode, timing=False):
+    def train(self, js, al, sd, mode, timing=False, compute_loss=False):
         self.calls.append((int(js[0]), int(js[-1]), len(al), len(sd)))
         for t in self.tables:
             t += float((self.rank + 1) * len(al))
@@ -83,6 +83,20 @@ def _worker(rank, world, port, q):
         Dd.touch_merge_(sep, sep_old)
         out["fused"] = both.numpy()
         out["separate"] = np.stack([x.numpy() for x in sep])
+        # shards whose job counts differ (rank 0: 10 jobs, rank 1: 6, merges every
+        # 4): both ranks must run max(3, 2) = 3 merge windows, or rank 0 would
+        # wait forever in its third all-reduce
+        tabs2 = [torch.zeros(3)]
+        eng2 = FakeEngine(tabs2, rank)
+        tr2 = Dd.ReplicaTrainer(eng2, tabs2, avg_every_jobs=4, merge="mean")
+        nj = 10 if rank == 0 else 6
+        tr2.train_epoch(np.arange(0, 2 * nj + 1, 2, dtype=np.int64), np.zeros(nj),
+                        np.zeros(nj, np.uint64))
+        out["uneven_calls"] = eng2.calls
+        out["uneven_averages"] = tr2.averages
+        out["uneven_tables"] = tabs2[0].numpy()
+        out["max_int"] = Dd.allreduce_max_int(5 + rank)
+        out["sum_float"] = Dd.allreduce_sum_float(0.5 * (rank + 1))
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -149,3 +163,29 @@ def test_touch_merge_fused_buffer_equals_per_table(results):
     for r in (0, 1):
         assert np.array_equal(results[r]["fused"], results[r]["separate"])
     assert np.array_equal(results[0]["fused"], results[1]["fused"])
+
+
+def test_uneven_shards_same_merge_count(results):
+    assert results[0]["uneven_calls"] == [(0, 8, 4, 4), (8, 16, 4, 4), (16, 20, 2, 2)]
+    assert results[1]["uneven_calls"] == [(0, 8, 4, 4), (8, 12, 2, 2)]
+    assert results[0]["uneven_averages"] == results[1]["uneven_averages"] == 3
+    # window adds: rank 0 4, 4, 2; rank 1 8, 4, 0 -> means 6, 4, 1 -> 11
+    assert np.array_equal(results[0]["uneven_tables"], results[1]["uneven_tables"])
+    assert np.allclose(results[0]["uneven_tables"], 11.0)
+
+
+def test_scalar_agreements(results):
+    for r in (0, 1):
+        assert results[r]["max_int"] == 6
+        assert results[r]["sum_float"] == 1.5
+
+
+def test_single_process_trainer_never_merges():
+    """world 1 (no process group): the windows train, no merge runs (the N = 1
+    bench carries no merge work)"""
+    import torch
+    t = [torch.zeros(2)]
+    eng = FakeEngine(t, 0)
+    tr = Dd.ReplicaTrainer(eng, t, avg_every_jobs=3, merge="touch")
+    tr.train_epoch(np.arange(0, 15, 2, dtype=np.int64), np.zeros(7), np.zeros(7, np.uint64))
+    assert tr.averages == 0 and len(eng.calls) == 3

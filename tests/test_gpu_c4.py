@@ -1,0 +1,138 @@
+"""GPU parity at BASELINE configs[3] ("C4"): V = 60,000 genes (Zipf 1.0 over
+ranks, the synthetic corpus of SURVEY.md 8(d)), dim 512, neg 15 -- tables of
+2 x 123 MB, larger than the L2s and a large share of the Infinity Cache, the
+HBM/MALL regime of the production kernel.
+
+  * sampler: effective words / examples of one production train() over 20 M
+    pairs equal the C oracle's count, and the records of job windows at the
+    start, middle and end of the corpus equal the oracle's bit for bit;
+  * sequential train() over 40 k pairs within 1e-5 relative of the C oracle;
+  * Hogwild (production grid) vs the oracle after 2 gensim iterations over
+    2 M pairs: held-in SGNS objective within 0.3 % (the oracle runs its
+    OpenMP Hogwild here, gensim's own workers=N mode: the sequential oracle
+    would take minutes at 50 kflop per example).
+"""
+import numpy as np
+import pytest
+
+from gene2vec_amd import _native as N
+from gene2vec_amd import engine as E
+from gene2vec_amd import synthetic as S
+from oracle import c_oracle as CO
+from oracle import sgns_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+V0, D, K = 60000, 512, 15
+
+
+@pytest.fixture(scope="module")
+def c4():
+    n = 20_000_000
+    pairs = S.zipf_gene_pairs(n, V0, 1.0, seed=20250114)
+    flat = pairs.reshape(-1)
+    del pairs
+    counts, first = E.count_ids(flat, V0)
+    order, remap = S.vocab_order(counts, first)
+    tok = remap[flat]
+    vc = counts[order].astype(np.int64)
+    return tok, vc, n
+
+
+def _init(V, seed=1):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    return ((rng.random((V, D)) - 0.5) / D).astype(np.float32)
+
+
+def test_c4_sampler_20m_bit_exact(c4):
+    tok, vc, n = c4
+    V = len(vc)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    sd = E.job_seeds(np.random.RandomState(1), len(js) - 1)
+    eng = E.SGNSEngine(V, D, K)
+    eng.set_vocab(vc, 1e-3)
+    eng.set_weights(_init(V), np.zeros((V, D), np.float32))
+    eng.set_corpus(tok, sent_len=2)
+    eng.train(js, E.job_alphas(js, n), sd, N.MODE_HOGWILD)
+    st = eng.read_stats()
+    off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
+    si, cum = CO.sample_int(vc, 1e-3), CO.make_cum_table(vc)
+    assert st["raw_words"] == 2 * n and st["jobs"] == len(js) - 1
+    assert st["examples"] == CO.count_records(tok, off, js, sd, si, True, cum, K)
+    nj = len(js) - 1
+    for j0 in (0, nj // 2, nj - 3):
+        w = js[j0:j0 + 4] - js[j0]
+        s0, s1 = js[j0], js[j0 + 3]
+        ref = CO.sample_records(tok[2 * s0:2 * s1], off[:s1 - s0 + 1], w, sd[j0:j0 + 3], si, True,
+                                cum, K)
+        got = eng.debug_sample(js[j0:j0 + 4], sd[j0:j0 + 3])
+        assert np.array_equal(got, ref), j0
+    g0, g1 = eng.get_weights()
+    assert np.isfinite(g0).all() and np.isfinite(g1).all() and np.abs(g1).max() > 0
+    eng.close()
+
+
+def test_c4_sequential_train_vs_oracle(c4):
+    tok, vc, _ = c4
+    V = len(vc)
+    n = 40000
+    t = tok[:2 * n]
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    al = E.job_alphas(js, n)
+    sd = E.job_seeds(np.random.RandomState(1), len(js) - 1)
+    syn0 = _init(V, 2)
+    eng = E.SGNSEngine(V, D, K)
+    eng.set_vocab(vc, 1e-3)
+    eng.set_weights(syn0, np.zeros((V, D), np.float32))
+    eng.set_corpus(t, sent_len=2)
+    eng.train(js, al, sd, N.MODE_SEQUENTIAL)
+    st = eng.read_stats()
+    g0, g1 = eng.get_weights()
+    eng.close()
+    a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
+    off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
+    ref = CO.train(t, off, js, al.astype(np.float32), sd, CO.sample_int(vc, 1e-3), True,
+                   CO.make_cum_table(vc), a0, a1, np.ones(V, np.float32), K)
+    assert (st["effective_words"], st["examples"]) == (ref["effective_words"], ref["examples"])
+    np.testing.assert_allclose(g0, a0, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(g1, a1, rtol=1e-5, atol=1e-6)
+
+
+def _objective(s0, s1, tok, vc, n_eval=20000, seed=99):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    n = len(tok) // 2
+    idx = rng.integers(0, n, n_eval)
+    c, j = tok[2 * idx], tok[2 * idx + 1]
+    p = vc.astype(np.float64) ** 0.75
+    negs = rng.choice(len(vc), size=(n_eval, K), p=p / p.sum())
+    return O.sgns_loss(s0, s1, c, j, negs)
+
+
+def test_c4_hogwild_objective_vs_oracle(c4):
+    tok, vc, _ = c4
+    V = len(vc)
+    n = 2_000_000
+    t = tok[:2 * n]
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    syn0 = _init(V, 3)
+    eng = E.SGNSEngine(V, D, K)
+    eng.set_vocab(vc, 1e-3)
+    assert eng.get_option(N.OPT_GRID) > 0
+    eng.set_weights(syn0, np.zeros((V, D), np.float32))
+    eng.set_corpus(t, sent_len=2)
+    a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
+    off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
+    si, cum = CO.sample_int(vc, 1e-3), CO.make_cum_table(vc)
+    rs_g, rs_c = np.random.RandomState(1), np.random.RandomState(1)
+    for _ in range(2):
+        al = E.job_alphas(js, n)
+        eng.train(js, al, E.job_seeds(rs_g, len(js) - 1), N.MODE_HOGWILD)
+        CO.train(t, off, js, al.astype(np.float32), E.job_seeds(rs_c, len(js) - 1), si, True,
+                 cum, a0, a1, np.ones(V, np.float32), K, nthreads=16, ld=D)
+    g0, g1 = eng.get_weights()
+    eng.close()
+    l_gpu = _objective(g0, g1, t, vc)
+    l_ref = _objective(a0, a1, t, vc)
+    l_init = _objective(syn0, np.zeros_like(a1), t, vc)
+    assert l_ref < 0.97 * l_init
+    assert abs(l_gpu - l_ref) / l_ref < 0.003, (l_gpu, l_ref, l_init)

@@ -1,0 +1,167 @@
+"""GPU: gensim 3.4's compute_loss ([ext] word2vec_inner.pyx fast_sentence_sg_neg:
+``f_dot = f_dot if d == 0 else -f_dot; _running_training_loss -= LOG_TABLE[...]``
+for every applied target; reset by every train() call; read back with
+``get_latest_training_loss()``), through the C ABI (G2V_FLAG_COMPUTE_LOSS).
+
+Bars:
+  * SEQUENTIAL: the float32 running sum of the C oracle in gensim's order,
+    within 1e-5 relative (the kernel's fp64 dot can round f to the other
+    side of a LUT cell boundary, the same tolerance as the tables' 1e-5);
+  * HOGWILD: at C2's vocabulary within 3 % (iteration 1) and 1.5 %
+    (iteration 2) of the sequential oracle's loss on the same jobs and seeds
+    (the tally prices each prediction before its update, so staleness shows
+    while the model learns fast; gensim's own workers>1 tally is a racy
+    read-modify-write of one float);
+  * tallying never changes the training (sequential tables bitwise equal).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from gene2vec_amd import _native as N
+from gene2vec_amd import engine as E
+from gene2vec_amd.word2vec import Word2Vec
+from oracle import c_oracle as CO
+from oracle import sgns_oracle as O
+from tests.conftest import GOLDEN
+from tests.helpers import crc_hash, vocab_from_ids, zipf_pairs
+
+pytestmark = pytest.mark.gpu
+
+
+def _zipf(n_pairs, V, D, seed=20250114):
+    pairs = zipf_pairs(n_pairs, V, seed=seed)
+    flat = pairs.reshape(-1)
+    _, remap, counts = vocab_from_ids(flat, V)
+    tok = remap[flat]
+    rng = np.random.Generator(np.random.PCG64(1))
+    syn0 = ((rng.random((len(counts), D)) - 0.5) / D).astype(np.float32)
+    return tok, counts, syn0
+
+
+def _run(tok, counts, syn0, K, sample, mode, compute_loss, iters=1, seg_jobs=0):
+    V, D = syn0.shape
+    n = len(tok) // 2
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    eng = E.SGNSEngine(V, D, K)
+    if seg_jobs:
+        eng.set_option(N.OPT_SEG_JOBS, seg_jobs)
+    eng.set_vocab(counts, sample)
+    eng.set_weights(syn0, np.zeros((V, D), np.float32))
+    eng.set_corpus(tok, sent_len=2)
+    rs = np.random.RandomState(1)
+    losses = []
+    for _ in range(iters):
+        eng.reset_loss()
+        eng.train(js, E.job_alphas(js, n), E.job_seeds(rs, len(js) - 1), mode,
+                  compute_loss=compute_loss)
+        losses.append(eng.read_stats()["training_loss"])
+    g0, g1 = eng.get_weights()
+    eng.close()
+    return losses, g0, g1
+
+
+def _oracle(tok, counts, syn0, K, sample, iters=1, nthreads=0):
+    V, D = syn0.shape
+    n = len(tok) // 2
+    off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
+    rs = np.random.RandomState(1)
+    losses = []
+    for _ in range(iters):
+        loss = np.zeros(1, np.float32) if not nthreads else None
+        CO.train(tok, off, js, E.job_alphas(js, n).astype(np.float32),
+                 E.job_seeds(rs, len(js) - 1), CO.sample_int(counts, sample), sample != 0,
+                 CO.make_cum_table(counts), a0, a1, np.ones(V, np.float32), K,
+                 nthreads=nthreads, loss=loss)
+        losses.append(None if loss is None else float(loss[0]))
+    return losses, a0, a1
+
+
+@pytest.mark.parametrize("D,K,seg_jobs", [(200, 5, 0), (200, 5, 3), (64, 15, 0)])
+def test_loss_sequential_equals_oracle(D, K, seg_jobs):
+    """two train() calls, each reset: the float32 running sum continues across
+    the segment launches of one call (seg_jobs = 3 splits 8 jobs)"""
+    tok, counts, syn0 = _zipf(40000, 2000, D)
+    got, g0, g1 = _run(tok, counts, syn0, K, 1e-3, N.MODE_SEQUENTIAL, True, iters=2,
+                       seg_jobs=seg_jobs)
+    ref, a0, a1 = _oracle(tok, counts, syn0, K, 1e-3, iters=2)
+    for x, y in zip(got, ref):
+        assert y > 0
+        assert abs(x - y) / y < 1e-5, (got, ref)
+    np.testing.assert_allclose(g1, a1, rtol=1e-5, atol=1e-6)
+
+
+def test_loss_tally_does_not_change_training():
+    tok, counts, syn0 = _zipf(20000, 1000, 200)
+    _, g0, g1 = _run(tok, counts, syn0, 5, 1e-3, N.MODE_SEQUENTIAL, True)
+    l_off, h0, h1 = _run(tok, counts, syn0, 5, 1e-3, N.MODE_SEQUENTIAL, False)
+    assert np.array_equal(g0, h0) and np.array_equal(g1, h1)
+    assert l_off == [0.0]
+
+
+def test_loss_hogwild_tracks_sequential():
+    """C2 vocabulary, 2 M pairs, 2 gensim iterations.  The running loss tallies
+    each example's prediction BEFORE its update, so it depends on how stale
+    the rows were: ~2,000 examples in flight see the rows of the epoch's fast
+    first phase late and pay a larger loss than workers=1 does (measured on
+    200 k pairs / V 3,000: +3.8 % in iteration 1, +3.1 % in iteration 2).
+    Bars: iteration 1 within 3 %, iteration 2 within 1.5 %."""
+    D, K = 200, 5
+    tok, counts, syn0 = _zipf(2_000_000, 24447, D)
+    got, g0, g1 = _run(tok, counts, syn0, K, 1e-3, N.MODE_HOGWILD, True, iters=2)
+    ref, _, _ = _oracle(tok, counts, syn0, K, 1e-3, iters=2)
+    print("hogwild loss", got, "sequential oracle", ref)
+    assert abs(got[0] - ref[0]) / ref[0] < 0.03, (got, ref)
+    assert abs(got[1] - ref[1]) / ref[1] < 0.015, (got, ref)
+    assert np.isfinite(g0).all() and np.isfinite(g1).all()
+
+
+@pytest.mark.parametrize("mode", [N.MODE_SEQUENTIAL, N.MODE_HOGWILD, N.MODE_MINIBATCH])
+def test_loss_step_explicit_golden(mode):
+    """explicit-negative step: SEQUENTIAL equals the oracle's float running sum;
+    the parallel modes sum the same terms in another order (Hogwild: disjoint
+    rows, so every term is the sequential one)"""
+    z = np.load(os.path.join(GOLDEN, "step_V60_D200_K5.npz"))
+    V, D = z["syn0"].shape
+    eng = E.SGNSEngine(V, D, 5)
+    eng.set_weights(z["syn0"], z["syn1neg"])
+    eng.reset_loss()
+    eng.step_explicit(z["center"], z["input"], z["negs"], float(z["alpha"]), mode,
+                      compute_loss=True)
+    got = eng.read_stats()["training_loss"]
+    loss = np.zeros(1, np.float32)
+    a0, a1 = z["syn0"].copy(), z["syn1neg"].copy()
+    CO.sgns_step_sequential(a0, a1, np.ones(V, np.float32), z["center"], z["input"], z["negs"],
+                            float(z["alpha"]), loss=loss)
+    if mode == N.MODE_SEQUENTIAL:
+        assert abs(got - loss[0]) / loss[0] < 1e-5
+    elif mode == N.MODE_MINIBATCH:
+        # every example reads the pre-step tables: the oracle's first-example
+        # terms of a fresh model on each example; same magnitude
+        assert 0.5 * loss[0] < got < 2.0 * loss[0]
+    else:
+        assert abs(got - loss[0]) / loss[0] < 0.05
+    eng.close()
+
+
+def test_word2vec_compute_loss_api(test_pairs):
+    """gensim 3.4 semantics: compute_loss per train() call, running loss reset
+    at the start of each call, get_latest_training_loss()"""
+    model = Word2Vec(test_pairs, size=200, window=1, min_count=1, workers=32, iter=1, sg=1,
+                     hashfxn=crc_hash, mode="sequential", compute_loss=True)
+    first = model.get_latest_training_loss()
+    voc = O.build_vocab(test_pairs, 1, 1e-3)
+    syn0, syn1, lockf = O.reset_weights(voc.index2word, 200, 1, crc_hash)
+    loss = np.zeros(1, np.float32)
+    O.train_epoch_sequential(O.sentences_to_ids(test_pairs, voc.word2index), voc, syn0, syn1,
+                             lockf, O.make_cum_table(voc.counts), 5, np.random.RandomState(1),
+                             loss=loss)
+    assert first > 0 and abs(first - loss[0]) / loss[0] < 1e-5
+    model.train(test_pairs, total_examples=model.corpus_count, epochs=model.iter)
+    assert model.get_latest_training_loss() == 0.0  # compute_loss defaults to False per call
+    model.train(test_pairs, total_examples=model.corpus_count, epochs=model.iter,
+                compute_loss=True)
+    assert 0 < model.get_latest_training_loss() < 2 * first

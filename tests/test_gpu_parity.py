@@ -325,8 +325,8 @@ def _eval_loss(syn0, syn1, tok, counts, K, n_eval=20000, seed=99):
 @pytest.mark.parametrize("D,K,seg_jobs", [(200, 5, 0), (512, 15, 0), (200, 5, 7)])
 def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs):
     """Hogwild GPU vs the sequential oracle on the same jobs/seeds: the SGNS
-    objective on held-in pairs must agree within 2 % (Hogwild reorders
-    updates; it is judged end-to-end)."""
+    objective on held-in pairs must agree within 0.5 % (Hogwild reorders
+    updates; it is judged end-to-end; measured 0.01-0.1 %)."""
     sample = 1e-3
     tok, counts, syn0 = _zipf_setup(200000, 3000, D, K, sample)
     V = len(counts)
@@ -352,7 +352,7 @@ def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs):
     l_ref = _eval_loss(a0, a1, tok, counts, K)
     l_init = _eval_loss(syn0, np.zeros_like(a1), tok, counts, K)
     assert l_ref < l_init * 0.95
-    assert abs(l_gpu - l_ref) / l_ref < 0.02, (l_gpu, l_ref, l_init)
+    assert abs(l_gpu - l_ref) / l_ref < 0.005, (l_gpu, l_ref, l_init)
 
 
 def test_train_counts_at_scale_bit_exact():
@@ -384,7 +384,7 @@ def test_train_counts_at_scale_bit_exact():
 
 def test_train_hogwild_full_vocab_tracks_oracle():
     """C2 vocabulary (V=24447, Zipf 1.0), 2M pairs, 2 gensim iterations:
-    the production kernel (striped hot rows, bounded grid) stays within 1 %
+    the production kernel (striped hot rows, bounded grid) stays within 0.3 %
     of the sequential oracle's objective (measured 0.01-0.1 %)."""
     D, K, sample = 200, 5, 1e-3
     tok, counts, syn0 = _zipf_setup(2_000_000, 24447, D, K, sample)
@@ -407,7 +407,7 @@ def test_train_hogwild_full_vocab_tracks_oracle():
     g0, g1 = eng.get_weights()
     l_gpu = _eval_loss(g0, g1, tok, counts, K, n_eval=50000)
     l_ref = _eval_loss(a0, a1, tok, counts, K, n_eval=50000)
-    assert abs(l_gpu - l_ref) / l_ref < 0.01, (l_gpu, l_ref)
+    assert abs(l_gpu - l_ref) / l_ref < 0.003, (l_gpu, l_ref)
 
 
 def test_striping_keeps_values_exact():
@@ -477,3 +477,44 @@ def test_sampler_at_c2_full_size_bit_exact():
         assert np.array_equal(got, ref), j0
     g0, g1 = eng.get_weights()
     assert np.isfinite(g0).all() and np.isfinite(g1).all() and np.abs(g1).max() > 0
+
+
+@pytest.mark.parametrize("V,zipf_s", [(300, 1.0), (2000, 1.0), (300, 0.0)])
+def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s):
+    """Small vocabularies, where every row is hot: the default grid is cut by
+    the staleness budget (waves x hottest-row updates per example), and the
+    Hogwild objective stays within 0.5 % of the sequential oracle after 3
+    gensim iterations (Zipf 1.0 and uniform genes)."""
+    D, K, sample = 200, 5, 1e-3
+    n = 300000
+    tok, counts, syn0 = _zipf_setup(n, V, D, K, sample, seed=31) if zipf_s else (None,) * 3
+    if not zipf_s:
+        rng = np.random.RandomState(31)
+        pairs = rng.randint(0, V, (n, 2)).astype(np.int32)
+        pairs[:, 1] = np.where(pairs[:, 1] == pairs[:, 0], (pairs[:, 0] + 1) % V, pairs[:, 1])
+        tok, counts = _corpus_from_pairs(pairs, V)
+        syn0 = ((np.random.Generator(np.random.PCG64(1)).random((len(counts), D)) - 0.5)
+                / D).astype(np.float32)
+    V = len(counts)
+    off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    eng = E.SGNSEngine(V, D, K)
+    eng.set_vocab(counts, sample)
+    grid = eng.get_option(N.OPT_GRID)
+    if zipf_s and V <= 300:
+        assert grid < 512, grid  # hotter than C4: fewer waves in flight
+    eng.set_weights(syn0, np.zeros((V, D), np.float32))
+    eng.set_corpus(tok, sent_len=2)
+    a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
+    rs_g, rs_c = np.random.RandomState(1), np.random.RandomState(1)
+    for _ in range(3):
+        al = E.job_alphas(js, n)
+        eng.train(js, al, E.job_seeds(rs_g, len(js) - 1), N.MODE_HOGWILD)
+        CO.train(tok, off, js, al.astype(np.float32), E.job_seeds(rs_c, len(js) - 1),
+                 CO.sample_int(counts, sample), True, CO.make_cum_table(counts), a0, a1,
+                 np.ones(V, np.float32), K)
+    g0, g1 = eng.get_weights()
+    eng.close()
+    l_gpu = _eval_loss(g0, g1, tok, counts, K)
+    l_ref = _eval_loss(a0, a1, tok, counts, K)
+    assert abs(l_gpu - l_ref) / l_ref < 0.005, (V, zipf_s, grid, l_gpu, l_ref)

@@ -27,7 +27,7 @@ def test_library_loads_and_exports_header():
         assert hasattr(L, s), s
         assert s in N.SIGNATURES, f"{s} missing from the ctypes signature table"
     assert set(N.SIGNATURES) == set(syms)
-    assert L.g2v_abi_version() == 1
+    assert L.g2v_abi_version() == N.ABI_VERSION == 2
 
 
 def test_error_path_without_gpu_is_loud():
@@ -47,7 +47,11 @@ def test_error_path_without_gpu_is_loud():
 
 
 @pytest.mark.parametrize("lengths", [[2] * 40, [2] * 12345, [2, 4, 0, 2, 3, 9997, 2, 10000, 1] * 3,
-                                     [], [0, 0, 0], [10000, 10000], [5000, 5000, 1]])
+                                     [], [0, 0, 0], [10000, 10000], [5000, 5000, 1],
+                                     # sentences over batch_words: a job each, and an
+                                     # empty first job when the first one is long
+                                     [10001], [25000, 2, 2], [2, 30000, 2, 10001, 0, 3],
+                                     [0, 10001], [10001, 10001, 10001]])
 def test_plan_jobs_matches_oracle(lengths):
     ref = O.plan_jobs(lengths)
     off = np.cumsum([0] + lengths).astype(np.int64)
@@ -56,11 +60,13 @@ def test_plan_jobs_matches_oracle(lengths):
     assert js.tolist() == expect
 
 
-def test_plan_jobs_uniform_and_limits():
+def test_plan_jobs_uniform_and_long_sentences():
     js = E.plan_jobs(n_sent=12345, sent_len=2)
     assert js.tolist() == [j[0] for j in O.plan_jobs([2] * 12345)] + [12345]
-    with pytest.raises(N.G2VError):
-        E.plan_jobs(sent_off=np.array([0, 10001], np.int64))
+    # [ext] _job_producer: a first sentence over batch_words queues the empty
+    # batch first (a job of its own, two model.random draws), then trains alone
+    assert E.plan_jobs(sent_off=np.array([0, 10001], np.int64)).tolist() == [0, 0, 1]
+    assert O.plan_jobs([10001]) == [(0, 0), (0, 1)]
 
 
 def test_job_alphas_and_seeds(golden):
@@ -104,7 +110,11 @@ def test_plan_jobs_fixed_length_equal_csr(n, sent_len):
     np.testing.assert_array_equal(csr, fixed)
 
 
-def test_plan_jobs_fixed_length_over_batch_words():
-    with pytest.raises(N.G2VError):
-        E.plan_jobs(n_sent=3, sent_len=N.BATCH_WORDS + 1)
-    np.testing.assert_array_equal(E.plan_jobs(n_sent=0, sent_len=N.BATCH_WORDS + 1), [0])
+@pytest.mark.parametrize("n", [0, 1, 3])
+def test_plan_jobs_fixed_length_over_batch_words(n):
+    L = N.BATCH_WORDS + 1
+    fixed = E.plan_jobs(n_sent=n, sent_len=L)
+    csr = E.plan_jobs(sent_off=np.arange(0, L * n + 1, L, dtype=np.int64))
+    np.testing.assert_array_equal(fixed, csr)
+    ref = O.plan_jobs([L] * n)
+    assert fixed.tolist() == ([ref[0][0]] + [j[1] for j in ref] if ref else [0])

@@ -13,7 +13,7 @@ import pytest
 from oracle import c_oracle as CO
 from oracle import sgns_oracle as O
 from tests.conftest import GOLDEN
-from tests.helpers import crc_hash
+from tests.helpers import crc_hash, long_sentence_corpus
 
 
 def test_reference_fixture_vocab(golden, test_pairs):
@@ -151,3 +151,79 @@ def test_c_records_match_numpy(test_pairs):
                                 voc.sample_int, True, cum, 5)
         ref = O.sample_job_records(ids, seed, voc.sample_int, True, cum, 5)
         assert rec.tolist() == [[c, j] + n for c, j, n in ref]
+
+
+# ---------------------------------------------------------------------------
+# compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally) and the
+# MAX_SENTENCE_LEN truncation of train_batch_sg
+# ---------------------------------------------------------------------------
+def test_log_table():
+    lt = O.log_table()
+    assert np.array_equal(lt, CO.log_table())
+    e = O.exp_table()
+    assert np.array_equal(lt, np.log(e.astype(np.float64)).astype(np.float32))
+    assert np.all(np.diff(lt) > 0) and np.all(lt < 0)
+    # the index int((0 + 6) * 83) = 498 of an untrained model: log(sigmoid(-0.024))
+    assert lt[498] == pytest.approx(np.log(1 / (1 + np.exp(0.024))), rel=1e-5)
+
+
+@pytest.mark.parametrize("sample", [0.0, 1e-3])
+def test_compute_loss_numpy_equals_c(test_pairs, sample):
+    """gensim's float32 running loss (workers=1 order) from both restatements,
+    over three train() calls continued (no reset between them)."""
+    voc = O.build_vocab(test_pairs, 1, sample)
+    ids = O.sentences_to_ids(test_pairs, voc.word2index)
+    tok = np.array([w for s in ids for w in s], np.int32)
+    off = np.cumsum([0] + [len(s) for s in ids]).astype(np.int64)
+    jobs = O.plan_jobs([len(s) for s in ids])
+    js = np.array([jobs[0][0]] + [j[1] for j in jobs], np.int64)
+    cum = O.make_cum_table(voc.counts)
+    n0, n1, nl = O.reset_weights(voc.index2word, 50, 1, crc_hash)
+    c0, c1 = n0.copy(), n1.copy()
+    l_np = np.zeros(1, np.float32)
+    l_c = np.zeros(1, np.float32)
+    rs_n, rs_c = np.random.RandomState(1), np.random.RandomState(1)
+    for _ in range(3):
+        O.train_epoch_sequential(ids, voc, n0, n1, nl, cum, 5, rs_n, sample=sample, loss=l_np)
+        al = np.array(O.job_alphas(jobs, len(ids)), np.float32)
+        sd = np.array(O.job_seeds(rs_c, len(jobs)), np.uint64)
+        CO.train(tok, off, js, al, sd, voc.sample_int, bool(sample), cum, c0, c1, nl, 5,
+                 loss=l_c)
+    assert l_np[0] == l_c[0] and l_c[0] > 0
+    np.testing.assert_allclose(c0, n0, rtol=1e-6, atol=1e-8)
+
+
+def test_compute_loss_first_example_is_log2_per_target():
+    """untrained syn1neg (zeros): every dot is 0 -> each applied target adds
+    -LOG_TABLE[498] = 0.7052...; a negative equal to the center is skipped"""
+    V, D, K = 10, 8, 5
+    syn0 = np.full((V, D), 0.01, np.float32)
+    syn1 = np.zeros((V, D), np.float32)
+    loss = np.zeros(1, np.float32)
+    negs = np.array([[1, 2, 0, 3, -1]], np.int32)  # 0 == center: skipped; -1 skipped
+    CO.sgns_step_sequential(syn0, syn1, np.ones(V, np.float32), np.array([0], np.int32),
+                            np.array([4], np.int32), negs, 0.025, loss=loss)
+    assert loss[0] == np.float32(-O.log_table()[498] * 4)
+
+
+@pytest.mark.parametrize("sample", [0.0, 1e-3])
+def test_long_sentence_truncation_numpy_equals_c(sample):
+    """sentences over batch_words: a job of their own (an empty job first when
+    the corpus starts with one), truncated at 10000 effective words"""
+    tok, off, counts = long_sentence_corpus()
+    lengths = np.diff(off).tolist()
+    jobs = O.plan_jobs(lengths)
+    assert jobs[0] == (0, 0)
+    js = np.array([jobs[0][0]] + [j[1] for j in jobs], np.int64)
+    seeds = np.array(O.job_seeds(np.random.RandomState(4), len(jobs)), np.uint64)
+    cum = O.make_cum_table(counts)
+    si = O.sample_int_from_counts(counts, sample)
+    rec = CO.sample_records(tok, off, js, seeds, si, sample != 0, cum, 5)
+    ref = []
+    sents = [tok[off[i]:off[i + 1]].tolist() for i in range(len(lengths))]
+    effs = []
+    for (s0, s1), sd in zip(jobs, seeds):
+        ref += O.sample_job_records(sents[s0:s1], int(sd), si, sample != 0, cum, 5)
+        effs.append(O.downsample_job(sents[s0:s1], si, int(sd), sample != 0)[2])
+    assert rec.tolist() == [[c, j] + n for c, j, n in ref]
+    assert max(effs) == 10000 and effs[0] == 0
