@@ -41,6 +41,26 @@ METRIC = "gene pairs/sec (SGNS dim200 neg5) at 1/2/4/8 MI355X + achieved GB/s"
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+def usable_cpus():
+    """(usable, os.cpu_count(), affinity, cgroup quota): the CPUs this process
+    may run on at once -- the GPU box shows the whole machine in
+    os.cpu_count() (256) but grants one GPU's share through the cgroup CPU
+    quota (cpu.max 1600000/100000 = 16 CPUs, measured)."""
+    host = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        aff = host
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return min(host, aff, quota or host), host, aff, quota
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -60,9 +80,10 @@ def parse():
                    help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
     p.add_argument("--cpu-threads", type=int, default=0,
-                   help="threads of the CPU baseline (0 = os.cpu_count(), every host core)")
+                   help="threads of the CPU baseline (0 = every CPU this process may use: "
+                        "min(os.cpu_count(), affinity, cgroup quota))")
     p.add_argument("--cpu-extra", action="store_true",
-                   help="also time the CPU baseline on 1 core and on 16 threads")
+                   help="also time the CPU baseline on 1 core and on os.cpu_count() threads")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-eval", action="store_true")
     p.add_argument("--no-gather-roof", action="store_true",
@@ -273,8 +294,8 @@ def main():
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         from oracle import c_oracle as CO
-        host_cores = os.cpu_count() or 1
-        ncpu = a.cpu_threads or host_cores
+        usable, host_cores, affinity, quota = usable_cpus()
+        ncpu = a.cpu_threads or usable
         ns = min(a.cpu_sample_pairs, n_pairs)
         jsc = E.plan_jobs(n_sent=ns, sent_len=2)
         off = np.arange(0, 2 * ns + 1, 2, dtype=np.int64)
@@ -293,19 +314,15 @@ def main():
             return time.perf_counter() - t
 
         dt = cpu_run(ncpu)
-        try:
-            affinity = len(os.sched_getaffinity(0))
-        except AttributeError:  # pragma: no cover
-            affinity = None
         cpu = {"value": round(ns / dt, 1), "unit": "pairs/s", "cores": ncpu, "kind": "port",
-               "host_cores": host_cores, "affinity_cores": affinity,
-               "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
+               "host_cores": host_cores, "affinity_cores": affinity, "cgroup_cpu_quota": quota,
                "sample": f"first {ns} pairs of the same corpus, 1 epoch, C oracle "
-                         f"(oracle/sgns_oracle.c) Hogwild OpenMP on {ncpu} threads "
-                         f"(os.cpu_count() = {host_cores}), rows padded to {ld_cpu} floats, "
+                         f"(oracle/sgns_oracle.c) Hogwild OpenMP on {ncpu} threads = every "
+                         f"CPU this process may use (os.cpu_count() {host_cores}, affinity "
+                         f"{affinity}, cgroup quota {quota}), rows padded to {ld_cpu} floats, "
                          f"{dt:.2f} s"}
         if a.cpu_extra:
-            for th in (16, 1):
+            for th in sorted({1, host_cores} - {ncpu}):
                 d = cpu_run(th)
                 cpu[f"value_{th}_threads"] = round(ns / d, 1)
 

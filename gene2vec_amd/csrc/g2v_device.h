@@ -97,11 +97,69 @@ struct Pow2<1> {
   static constexpr int v = 1;
 };
 
-__device__ __forceinline__ double shfl_xor_d(double v, int m) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __shfl_xor((int)(b & 0xffffffffLL), m, 64);
-  const int hi = __shfl_xor((int)(b >> 32), m, 64);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+// Cross-lane exchanges without LDS (no ds_bpermute): gfx950's
+// v_permlane32_swap / v_permlane16_swap for the lane masks 32 and 16, DPP
+// (row_ror:8, row_half_mirror, quad_perm) inside a row for 8, 4, 2, 1.  The
+// partner of lane l at mask m is l^m, except m = 4 where row_half_mirror pairs
+// l with l^7 (an involution that also flips bit 2: every butterfly below only
+// needs "partner differs in bit m, later stages cover the rest").
+__device__ __forceinline__ uint32_t lo32(double v) {
+  return (uint32_t)(__double_as_longlong(v) & 0xffffffffLL);
+}
+__device__ __forceinline__ uint32_t hi32(double v) {
+  return (uint32_t)((unsigned long long)__double_as_longlong(v) >> 32);
+}
+__device__ __forceinline__ double mk_d(uint32_t lo, uint32_t hi) {
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+template <int M>
+struct DppCtrl;
+template <>
+struct DppCtrl<8> { static constexpr int v = 0x128; };  // row_ror:8   -> l ^ 8
+template <>
+struct DppCtrl<4> { static constexpr int v = 0x141; };  // row_half_mirror -> l ^ 7
+template <>
+struct DppCtrl<2> { static constexpr int v = 0x4e; };   // quad_perm [2,3,0,1] -> l ^ 2
+template <>
+struct DppCtrl<1> { static constexpr int v = 0xb1; };   // quad_perm [1,0,3,2] -> l ^ 1
+
+template <int M>
+__device__ __forceinline__ double dpp_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)lo32(v), DppCtrl<M>::v, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)hi32(v), DppCtrl<M>::v, 0xf, 0xf, false);
+  return mk_d((uint32_t)lo, (uint32_t)hi);
+}
+
+// Lanes with bit M clear get a + partner's a, lanes with bit M set get
+// b + partner's b (one butterfly step carrying two values, keeping one).
+template <int M>
+__device__ __forceinline__ double xchg_pair(double a, double b, int lane) {
+  if constexpr (M == 32 || M == 16) {
+    // swap the upper 32 lanes of a with the lower 32 of b (M = 32), or the odd
+    // 16-lane rows of a with the even rows of b (M = 16): afterwards the two
+    // registers hold, lane for lane, the two addends of the wanted sum
+    auto slo = M == 32 ? __builtin_amdgcn_permlane32_swap(lo32(a), lo32(b), false, false)
+                       : __builtin_amdgcn_permlane16_swap(lo32(a), lo32(b), false, false);
+    auto shi = M == 32 ? __builtin_amdgcn_permlane32_swap(hi32(a), hi32(b), false, false)
+                       : __builtin_amdgcn_permlane16_swap(hi32(a), hi32(b), false, false);
+    return mk_d(slo[0], shi[0]) + mk_d(slo[1], shi[1]);
+  } else {
+    const bool up = (lane & M) != 0;
+    const double send = up ? a : b;
+    const double keep = up ? b : a;
+    return keep + dpp_d<M>(send);
+  }
+}
+
+// every lane: x + partner's x at mask M
+template <int M>
+__device__ __forceinline__ double xsum_d(double x) {
+  if constexpr (M == 32 || M == 16) {
+    return xchg_pair<M>(x, x, 0);
+  } else {
+    return x + dpp_d<M>(x);
+  }
 }
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
@@ -112,14 +170,39 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
 }
 
 __device__ __forceinline__ double wave_allreduce_d(double v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_d(v, m);
+  v = xsum_d<32>(v);
+  v = xsum_d<16>(v);
+  v = xsum_d<8>(v);
+  v = xsum_d<4>(v);
+  v = xsum_d<2>(v);
+  v = xsum_d<1>(v);
   return v;
 }
 
-// Sum NT per-lane values over the 64 lanes: value-halving xor butterfly (each
-// exchange step halves the values a lane carries), then a plain butterfly on
-// the last one; the NT totals end up wave-uniform.
+// one value-halving butterfly stage over the masks 32, 16, ..., 1 (index S)
+template <int S, int H, int P>
+__device__ __forceinline__ void halve_stage(double (&x)[P], int lane) {
+  constexpr int M = 32 >> S;
+#pragma unroll
+  for (int i = 0; i < H; ++i) x[i] = xchg_pair<M>(x[i], x[i + H], lane);
+}
+
+template <int S, int P>
+__device__ __forceinline__ void halve_all(double (&x)[P], int lane) {
+  constexpr int H = P >> (S + 1);  // values kept after this stage
+  if constexpr (H >= 1) {
+    halve_stage<S, H, P>(x, lane);
+    halve_all<S + 1, P>(x, lane);
+  } else if constexpr (S <= 5) {
+    x[0] = xsum_d<(32 >> S)>(x[0]);
+    halve_all<S + 1, P>(x, lane);
+  }
+}
+
+// Sum NT per-lane values over the 64 lanes: value-halving butterfly (each
+// stage exchanges half of the values a lane carries and keeps the other
+// half), then a plain butterfly on the last one; the NT totals end up
+// wave-uniform.
 template <int NT>
 __device__ __forceinline__ void wave_reduce_multi(const double (&in)[NT], double (&out)[NT],
                                                   int lane) {
@@ -128,21 +211,9 @@ __device__ __forceinline__ void wave_reduce_multi(const double (&in)[NT], double
   double x[P];
 #pragma unroll
   for (int i = 0; i < P; ++i) x[i] = (i < NT) ? in[i] : 0.0;
-  int m = 32;
-#pragma unroll
-  for (int h = P / 2; h >= 1; h >>= 1) {
-    const bool up = (lane & m) != 0;
-#pragma unroll
-    for (int i = 0; i < h; ++i) {
-      const double send = up ? x[i] : x[i + h];
-      const double keep = up ? x[i + h] : x[i];
-      x[i] = keep + shfl_xor_d(send, m);
-    }
-    m >>= 1;
-  }
-#pragma unroll
-  for (; m >= 1; m >>= 1) x[0] += shfl_xor_d(x[0], m);
-  // value v lives in lanes whose halving bits spell v
+  halve_all<0, P>(x, lane);
+  // value v lives in lanes whose halving bits spell v: bit h of v <-> lane
+  // bit (32 >> stage)
 #pragma unroll
   for (int v = 0; v < NT; ++v) {
     int src = 0, mm = 32;

@@ -64,11 +64,13 @@ def _u32_sample(sample_int):
 
 
 def train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum, syn0,
-          syn1neg, lockf, K, nthreads=0, loss=None, ld=None):
+          syn1neg, lockf, K, nthreads=0, loss=None, ld=None, loss_exact=None):
     """In-place training of syn0/syn1neg ([V][D] float32 C-order).
     nthreads == 0: sequential (workers=1 order); > 0: OpenMP Hogwild.
     loss: None, or a float32 array of one element holding gensim's running
-    training loss (compute_loss=True), continued in place (sequential only).
+    training loss (compute_loss=True), continued in place (sequential only);
+    loss_exact: None, or a float64 array of one element: the same terms
+    added in double (sequential only).
     ld: row stride in floats for the training copy (Hogwild: a multiple of 16
     keeps each row on cache lines of its own, so threads updating neighbouring
     hot rows do not falsely share lines); None = D, in place."""
@@ -80,16 +82,16 @@ def train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, c
         p0[:, :D] = syn0
         p1[:, :D] = syn1neg
         st = _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum,
-                    p0, p1, lockf, K, nthreads, loss, ld, D)
+                    p0, p1, lockf, K, nthreads, loss, ld, D, loss_exact)
         syn0[:] = p0[:, :D]
         syn1neg[:] = p1[:, :D]
         return st
     return _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum,
-                  syn0, syn1neg, lockf, K, nthreads, loss, D, D)
+                  syn0, syn1neg, lockf, K, nthreads, loss, D, D, loss_exact)
 
 
 def _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, cum, syn0,
-           syn1neg, lockf, K, nthreads, loss, ld, D):
+           syn1neg, lockf, K, nthreads, loss, ld, D, loss_exact=None):
     tok = np.ascontiguousarray(tok, dtype=np.int32)
     sent_off = np.ascontiguousarray(sent_off, dtype=np.int64)
     job_sent = np.ascontiguousarray(job_sent, dtype=np.int64)
@@ -107,12 +109,15 @@ def _train(tok, sent_off, job_sent, job_alpha, job_seed, sample_int, sample_on, 
             _p(si), C.c_int(int(bool(sample_on))), _p(cum), C.c_int32(V), _p(syn0), _p(syn1neg),
             _p(lockf), C.c_int64(ld), C.c_int32(D), C.c_int32(K)]
     if nthreads and nthreads > 0:
-        assert loss is None, "the oracle tallies the loss in sequential order only"
+        assert loss is None and loss_exact is None, \
+            "the oracle tallies the loss in sequential order only"
         lib().orc_train_hogwild(*args, C.c_int(nthreads), _p(stats))
     else:
         if loss is not None:
             assert loss.dtype == np.float32 and loss.size == 1
-        lib().orc_train_sequential(*args, _p(stats), _p(loss))
+        if loss_exact is not None:
+            assert loss_exact.dtype == np.float64 and loss_exact.size == 1
+        lib().orc_train_sequential(*args, _p(stats), _p(loss), _p(loss_exact))
     return dict(raw_words=int(stats[0]), effective_words=int(stats[1]), examples=int(stats[2]),
                 jobs=int(stats[3]))
 

@@ -117,12 +117,13 @@ static inline void saxpy(float g, const float *x, float *y, int D) {
 
 /* [ext] fast_sentence_sg_neg; returns the advanced LCG state.  negs != NULL:
  * explicit negatives (-1 = skipped) replace the LCG/bisect draw.  loss != NULL
- * (compute_loss): *loss -= LOG_TABLE[int((+-f + 6) * 83)] per applied target,
- * in float, in gensim's order. */
+ * (compute_loss): loss[0] -= LOG_TABLE[int((+-f + 6) * 83)] per applied target,
+ * in float, in gensim's order; loss_exact != NULL: the same terms summed in
+ * double (gensim's float running sum loses whole terms once it passes ~1e6). */
 static uint64_t sg_neg(int K, const uint32_t *cum, int32_t V, float *syn0, float *syn1neg,
                        int64_t ld, int D, int32_t word_index, int32_t word2_index, float alpha,
                        float *work, uint64_t nr, const float *lockf, const int32_t *negs,
-                       float *loss) {
+                       float *loss, double *loss_exact) {
     float *l1 = syn0 + (int64_t)word2_index * ld;
     memset(work, 0, sizeof(float) * D);
     for (int d = 0; d <= K; d++) {
@@ -145,9 +146,11 @@ static uint64_t sg_neg(int K, const uint32_t *cum, int32_t V, float *syn0, float
         float *row = syn1neg + (int64_t)t * ld;
         float f = dsdot(l1, row, D);
         if (f <= -MAX_EXP || f >= MAX_EXP) continue;
-        if (loss) {
+        if (loss || loss_exact) {
             const float fl = d == 0 ? f : -f;
-            *loss = *loss - g_log_table[(int)((fl + MAX_EXP) * LUT_SCALE)];
+            const float term = g_log_table[(int)((fl + MAX_EXP) * LUT_SCALE)];
+            if (loss) *loss = *loss - term;
+            if (loss_exact) *loss_exact -= (double)term;
         }
         f = g_exp_table[(int)((f + MAX_EXP) * LUT_SCALE)];
         float g = (label - f) * alpha;
@@ -166,7 +169,7 @@ static int64_t train_job(const int32_t *tok, const int64_t *sent_off, int64_t s0
                          const uint32_t *cum, int32_t V, float *syn0, float *syn1neg,
                          const float *lockf, int64_t ld, int D, int K, float *work, int32_t *kept,
                          int32_t *sidx, int64_t *n_ex, int32_t *rec_out, int64_t rec_cap,
-                         int do_train, float *loss) {
+                         int do_train, float *loss, double *loss_exact) {
     int32_t eff = 0, nsent = 0;
     sidx[0] = 0;
     for (int64_t s = s0; s < s1; s++) {
@@ -196,7 +199,7 @@ static int64_t train_job(const int32_t *tok, const int64_t *sent_off, int64_t s0
                 if (j == i) continue;
                 if (do_train) {
                     nr = sg_neg(K, cum, V, syn0, syn1neg, ld, D, kept[i], kept[j], alpha, work,
-                                nr, lockf, NULL, loss);
+                                nr, lockf, NULL, loss, loss_exact);
                 } else if (rec_out && nex < rec_cap) {
                     int32_t *r = rec_out + nex * (K + 2);
                     r[0] = kept[i];
@@ -216,12 +219,14 @@ static int64_t train_job(const int32_t *tok, const int64_t *sent_off, int64_t s0
 }
 
 /* stats[0]=raw words, [1]=effective words, [2]=examples, [3]=jobs.  loss:
- * NULL, or gensim's float running training loss, continued in place */
+ * NULL, or gensim's float running training loss, continued in place;
+ * loss_exact: NULL, or the same terms added in double */
 void orc_train_sequential(const int32_t *tok, const int64_t *sent_off, const int64_t *job_sent,
                           int64_t n_jobs, const float *job_alpha, const uint64_t *job_seed,
                           const uint32_t *sample_int, int sample_on, const uint32_t *cum,
                           int32_t V, float *syn0, float *syn1neg, const float *lockf, int64_t ld,
-                          int32_t D, int32_t K, int64_t *stats, float *loss) {
+                          int32_t D, int32_t K, int64_t *stats, float *loss,
+                          double *loss_exact) {
     ensure_exp();
     float *work = (float *)malloc(sizeof(float) * D);
     int32_t *kept = (int32_t *)malloc(sizeof(int32_t) * MAX_SENTENCE_LEN);
@@ -231,7 +236,7 @@ void orc_train_sequential(const int32_t *tok, const int64_t *sent_off, const int
         int64_t nex = 0;
         eff += train_job(tok, sent_off, job_sent[j], job_sent[j + 1], job_alpha[j], job_seed[j],
                          sample_int, sample_on, cum, V, syn0, syn1neg, lockf, ld, D, K, work, kept,
-                         sidx, &nex, NULL, 0, 1, loss);
+                         sidx, &nex, NULL, 0, 1, loss, loss_exact);
         ex += nex;
     }
     if (stats) {
@@ -265,7 +270,7 @@ void orc_train_hogwild(const int32_t *tok, const int64_t *sent_off, const int64_
             int64_t nex = 0;
             eff += train_job(tok, sent_off, job_sent[j], job_sent[j + 1], job_alpha[j],
                              job_seed[j], sample_int, sample_on, cum, V, syn0, syn1neg, lockf, ld,
-                             D, K, work, kept, sidx, &nex, NULL, 0, 1, NULL);
+                             D, K, work, kept, sidx, &nex, NULL, 0, 1, NULL, NULL);
             ex += nex;
         }
         free(work);
@@ -295,7 +300,7 @@ int64_t orc_sample_records(const int32_t *tok, const int64_t *sent_off, const in
         int64_t cap = rec_cap - total;
         train_job(tok, sent_off, job_sent[j], job_sent[j + 1], 0.0f, job_seed[j], sample_int,
                   sample_on, cum, V, NULL, NULL, NULL, 0, 0, K, NULL, kept, sidx, &nex,
-                  cap > 0 ? dst : NULL, cap, 0, NULL);
+                  cap > 0 ? dst : NULL, cap, 0, NULL, NULL);
         total += nex;
     }
     free(kept);
@@ -311,6 +316,6 @@ void orc_sgns_step_sequential(float *syn0, float *syn1neg, const float *lockf, i
     float *work = (float *)malloc(sizeof(float) * D);
     for (int64_t e = 0; e < n; e++)
         sg_neg(K, NULL, 0, syn0, syn1neg, ld, D, center[e], input[e], alpha, work, 0, lockf,
-               negs + e * K, loss);
+               negs + e * K, loss, NULL);
     free(work);
 }

@@ -1,0 +1,65 @@
+"""Per-example HBM traffic of k_sgns_atomic from the PMC passes of
+scripts/profile_round.sh (rocprofv3 --pmc CSVs + the bench JSON of the same
+10 M-pair run).  FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B
+per-lane reads, MI355X_MICROARCH.md 'HBM'); WRITE_SIZE is exact for float
+atomics.  Prints the JSON bench.py reads as --traffic-json."""
+import csv
+import glob
+import json
+import os
+import sys
+
+KERNEL = "k_sgns_atomic"
+
+
+def counters(d):
+    tot = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if KERNEL not in row["Kernel_Name"]:
+                    continue
+                k = row["Counter_Name"]
+                tot[k] = tot.get(k, 0.0) + float(row["Counter_Value"])
+    return tot
+
+
+def bench_line(log):
+    for line in open(log):
+        if line.startswith("{"):
+            return json.loads(line)
+    raise SystemExit(f"no bench JSON in {log}")
+
+
+def main(out):
+    c = {}
+    for i in range(1, 5):
+        c.update(counters(os.path.join(out, f"p{i}")))
+    b = bench_line(os.path.join(out, "p1.log"))
+    ex = b["effective_examples"]
+    launches = max(1, round(ex / (b["roofline"]["algorithmic_bytes_per_launch"]
+                                  / b["roofline"]["bytes_per_example"])))
+    fetch = 2.0 * c["FETCH_SIZE"] * 1024 / ex
+    write = c["WRITE_SIZE"] * 1024 / ex
+    hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
+    bpe = b["roofline"]["bytes_per_example"]
+    cfg = b["config"]
+    res = {
+        "vocab": cfg["vocab"], "dim": cfg["dim"], "negative": cfg["negative"],
+        "sample": cfg["sample"], "zipf": 1.0, "kernel": KERNEL,
+        "method": "rocprofv3 --pmc, one counter group per run (scripts/profile_round.sh), "
+                  "10 M-pair bench; FETCH_SIZE x2 (gfx950 16-B/lane read correction), "
+                  "WRITE_SIZE as is (KB units); summed over the SGNS launches / examples",
+        "fetch_bytes_per_example": fetch, "write_bytes_per_example": write,
+        "atomic_requests_per_example": c.get("TCC_EA0_ATOMIC_sum", 0.0) / ex,
+        "l2_hit_rate_incl_atomic_misses": hit / (hit + miss) if hit + miss else None,
+        "examples_per_launch": ex / launches,
+        "hbm_bytes_per_launch": (fetch + write) * ex / launches,
+        "algorithmic_bytes_per_example": bpe,
+        "traffic_over_algorithmic": (fetch + write) / bpe,
+    }
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
