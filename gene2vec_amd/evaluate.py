@@ -91,7 +91,10 @@ def target_function(emb_w2v_file, gmt_file=None, pathways=None, strict=True, dev
                 raise ZeroDivisionError("pathway with fewer than 2 in-vocabulary genes "
                                         "(src/evaluation_target_function.py:40)")
             continue
-        paths.append(np.float32(_f32_sum(sims[n0:n1]) / np.float32(n1 - n0)))
+        # sum(tmp_arr)/len(tmp_arr) (:40): float32 adds, then a float32 scalar
+        # over a Python int, which NumPy 1.x (the gensim 3.4 era) promotes to
+        # float64; the mean of means (:54-55) and the ratio stay float64
+        paths.append(np.float64(_f32_sum(sims[n0:n1])) / (n1 - n0))
     # denominator: random.seed(35); shuffle; first 1000 genes, all pairs
     rng = random.Random(35)
     shuffled = list(gene_list)
@@ -99,9 +102,9 @@ def target_function(emb_w2v_file, gmt_file=None, pathways=None, strict=True, dev
     top = [idx[w] for w in shuffled[:1000]]
     ra, rb = zip(*itertools.combinations(top, 2)) if len(top) > 1 else ((), ())
     rsims = cosine_pairs(kv, ra, rb, device)
-    path_mean = np.float32(_f32_sum(paths) / np.float32(len(paths)))
-    rand_mean = np.float32(_f32_sum(rsims) / np.float32(len(rsims)))
-    ratio = np.float32(path_mean / rand_mean)
+    path_mean = np.float64(sum(paths)) / len(paths)
+    rand_mean = np.float64(_f32_sum(rsims)) / len(rsims)
+    ratio = path_mean / rand_mean
     if verbose:
         print("------------")
         print(emb_w2v_file)

@@ -1,7 +1,9 @@
 """Restatement of src/evaluation_target_function.py on numpy/gensim semantics
 -- TEST INFRASTRUCTURE ONLY.  wv.similarity = float32 dot of gensim
 unitvec(v) = sscal(1/snrm2(v), v); Python sum() of float32 scalars is a
-sequential float32 accumulation.  Parity unpinned (gensim absent)."""
+sequential float32 accumulation; dividing that float32 by a Python int is
+float64 under NumPy 1.x (the gensim 3.4 era), so the pathway means, their
+mean and the ratio are float64.  Parity unpinned (gensim absent)."""
 import itertools
 import random
 
@@ -35,7 +37,7 @@ def target_function(words, vecs, pathways):
         for x, y in itertools.combinations(genes, 2):
             arr = np.float32(arr + similarity(vecs, idx[x], idx[y]))
             cnt += 1
-        paths.append(np.float32(arr / np.float32(cnt)))  # ZeroDivision -> inf/nan in numpy
+        paths.append(np.float64(arr) / cnt)  # cnt == 0: nan (the reference raises: sum([]) is int 0)
     gl = list(words)
     random.seed(35)
     random.shuffle(gl)
@@ -44,9 +46,9 @@ def target_function(words, vecs, pathways):
     for x, y in itertools.combinations(gl[:1000], 2):
         rs = np.float32(rs + similarity(vecs, idx[x], idx[y]))
         cnt += 1
-    pm = np.float32(0)
+    pm = 0.0
     for p in paths:
-        pm = np.float32(pm + p)
-    pm = np.float32(pm / np.float32(len(paths)))
-    rm = np.float32(rs / np.float32(cnt))
-    return float(pm), float(rm), float(np.float32(pm / rm))
+        pm = pm + p
+    pm = pm / len(paths)
+    rm = np.float64(rs) / cnt
+    return float(pm), float(rm), float(pm / rm)
