@@ -182,12 +182,17 @@ struct g2v_ctx {
 // updates the others do not see yet; the rows that suffer are the hottest
 // syn1neg rows, which take u_max = max_r(K p_neg(r) + p_tok(r)) updates per
 // example (p_neg: the unigram^0.75 table, p_tok: the downsampled token
-// distribution).  Measured: 2 workgroups (8 waves) per CU track the sequential
-// oracle at C2 (V 24,447 Zipf, u_max 0.12) and at C4 (V 60,000, K 15, u_max
-// 0.27) through the 10-iteration schedule, while 3 per CU diverge at C2.  So
-// the grid is 2 workgroups per CU, cut further where a vocabulary is hotter
-// than C4: waves x u_max <= kStaleBudget (= 2,048 waves x 0.267).
-constexpr double kStaleBudget = 546.0;
+// distribution).  The reference's sawtooth (alpha back to 0.025 every
+// train() call on an already trained model) is where too many waves blow up.
+// Measured on MI355X (profiles/r02_stale_grid.md):
+//   C2 (V 24,447 Zipf, K 5, u_max 0.122): 512 workgroups (2,048 waves,
+//     waves x u_max = 249) track the oracle through the 10-iteration
+//     schedule; 768 (373) diverge in iteration 3;
+//   C4 (V 60,000, D 512, K 15, u_max 0.267): 512 (546) diverge in the second
+//     epoch of a 10 M-pair corpus, 256 (273) and 128 match the CPU oracle.
+// So waves x u_max <= kStaleBudget = C2's 249, and never more than 2
+// workgroups per CU.
+constexpr double kStaleBudget = 250.0;
 
 static int default_grid(int cus, int K, int nv, double u_max) {
   int g = std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);

@@ -12,7 +12,7 @@ import sys
 import time
 import zlib
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.environ.get("G2V_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
@@ -37,6 +37,8 @@ def main():
     p.add_argument("--sample", type=float, default=1e-3)
     p.add_argument("--reps", type=int, default=2)
     p.add_argument("--configs", nargs="+", default=["ld=224"])
+    p.add_argument("--epochs-eval", action="store_true",
+                   help="print the held-in objective after every epoch")
     a = p.parse_args()
     import torch
 
@@ -79,6 +81,7 @@ def main():
             eng.set_option(N.OPT_SEG_JOBS, int(cfg["seg"]))
         if "dbg" in cfg:
             eng.set_option(N.OPT_DEBUG_WRITE, int(cfg["dbg"]))
+        mode = N.MODE_SEQUENTIAL if cfg.get("mode") == "seq" else N.MODE_HOGWILD
         stream = torch.cuda.Stream(dev)
         eng.set_stream(stream.cuda_stream)
         tables = torch.zeros((2, V, ld), dtype=torch.float32, device=dev)
@@ -88,15 +91,25 @@ def main():
         eng.set_corpus_device(tok_d.data_ptr(), tok_d.numel(), sent_len=2, keepalive=tok_d)
         rs = np.random.RandomState(1)
         rates = []
+        per_epoch = []
         for rep in range(a.reps):
-            eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD, timing=True)
+            eng.train(js, al, E.job_seeds(rs, len(js) - 1), mode, timing=True)
             st = eng.read_stats()
             rates.append(st["examples"] / (st["sgns_kernel_ms"] / 1e3))
+            if a.epochs_eval:
+                torch.cuda.synchronize()
+                per_epoch.append(round(O.sgns_loss(tables[0, :, :D].cpu().numpy(),
+                                                   tables[1, :, :D].cpu().numpy(), ec, ej,
+                                                   enegs), 4))
         torch.cuda.synchronize()
         s0 = tables[0, :, :D].cpu().numpy()
         s1 = tables[1, :, :D].cpu().numpy()
         loss = O.sgns_loss(s0, s1, ec, ej, enegs)
-        print(json.dumps({"config": text, "ld": ld, "grid": eng.get_option(N.OPT_GRID),
+        try:
+            grid = eng.get_option(N.OPT_GRID)
+        except AttributeError:  # round-1 library
+            grid = None
+        print(json.dumps({"config": text, "ld": ld, "grid": grid, "per_epoch": per_epoch,
                           "ex_per_s": [round(r / 1e6, 2) for r in rates],
                           "launch_ms": round(st["sgns_kernel_ms"] / max(1, st["launches"]), 3),
                           "heldin_loss_after": round(loss, 4)}), flush=True)

@@ -8,9 +8,12 @@ HBM/MALL regime of the production kernel.
     start, middle and end of the corpus equal the oracle's bit for bit;
   * sequential train() over 40 k pairs within 1e-5 relative of the C oracle;
   * Hogwild (production grid) vs the oracle after 2 gensim iterations over
-    2 M pairs: held-in SGNS objective within 0.3 % (the oracle runs its
-    OpenMP Hogwild here, gensim's own workers=N mode: the sequential oracle
-    would take minutes at 50 kflop per example).
+    10 M pairs: held-in SGNS objective within 0.3 % after each iteration (the
+    oracle runs its OpenMP Hogwild here, gensim's own workers=N mode: the
+    sequential oracle would take minutes at 50 kflop per example).  The
+    second iteration restarts alpha at 0.025 on a trained model (the
+    reference's sawtooth): 512 workgroups diverged there (4.7 vs 3.61) while
+    the 2 M-pair version of this test still passed, so the corpus is long.
 """
 import numpy as np
 import pytest
@@ -111,7 +114,7 @@ def _objective(s0, s1, tok, vc, n_eval=20000, seed=99):
 def test_c4_hogwild_objective_vs_oracle(c4):
     tok, vc, _ = c4
     V = len(vc)
-    n = 2_000_000
+    n = 10_000_000
     t = tok[:2 * n]
     js = E.plan_jobs(n_sent=n, sent_len=2)
     syn0 = _init(V, 3)
@@ -124,15 +127,15 @@ def test_c4_hogwild_objective_vs_oracle(c4):
     off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
     si, cum = CO.sample_int(vc, 1e-3), CO.make_cum_table(vc)
     rs_g, rs_c = np.random.RandomState(1), np.random.RandomState(1)
-    for _ in range(2):
+    l_init = _objective(syn0, np.zeros_like(a1), t, vc)
+    for it in range(2):
         al = E.job_alphas(js, n)
         eng.train(js, al, E.job_seeds(rs_g, len(js) - 1), N.MODE_HOGWILD)
         CO.train(t, off, js, al.astype(np.float32), E.job_seeds(rs_c, len(js) - 1), si, True,
                  cum, a0, a1, np.ones(V, np.float32), K, nthreads=16, ld=D)
-    g0, g1 = eng.get_weights()
+        g0, g1 = eng.get_weights()
+        l_gpu = _objective(g0, g1, t, vc)
+        l_ref = _objective(a0, a1, t, vc)
+        assert l_ref < 0.5 * l_init
+        assert abs(l_gpu - l_ref) / l_ref < 0.003, (it, l_gpu, l_ref, l_init)
     eng.close()
-    l_gpu = _objective(g0, g1, t, vc)
-    l_ref = _objective(a0, a1, t, vc)
-    l_init = _objective(syn0, np.zeros_like(a1), t, vc)
-    assert l_ref < 0.97 * l_init
-    assert abs(l_gpu - l_ref) / l_ref < 0.003, (l_gpu, l_ref, l_init)
