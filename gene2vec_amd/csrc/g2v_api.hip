@@ -101,7 +101,7 @@ struct g2v_ctx {
   int64_t ld = 0;
   int cus = 0, sgns_grid = 0;
   bool grid_user = false;       // G2V_OPT_GRID set explicitly
-  double u_max = 0.0;           // hottest-row updates per example (set_vocab)
+  double u_max = 0.0;           // hottest row's negative draws per example (set_vocab)
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
@@ -179,20 +179,19 @@ struct g2v_ctx {
 };
 
 // Hogwild staleness bound.  Every wave in flight holds one example whose
-// updates the others do not see yet; the rows that suffer are the hottest
-// syn1neg rows, which take u_max = max_r(K p_neg(r) + p_tok(r)) updates per
-// example (p_neg: the unigram^0.75 table, p_tok: the downsampled token
-// distribution).  The reference's sawtooth (alpha back to 0.025 every
-// train() call on an already trained model) is where too many waves blow up.
-// Measured on MI355X (profiles/r02_stale_grid.md):
-//   C2 (V 24,447 Zipf, K 5, u_max 0.122): 512 workgroups (2,048 waves,
-//     waves x u_max = 249) track the oracle through the 10-iteration
-//     schedule; 768 (373) diverge in iteration 3;
-//   C4 (V 60,000, D 512, K 15, u_max 0.267): 512 (546) diverge in the second
-//     epoch of a 10 M-pair corpus, 256 (273) and 128 match the CPU oracle.
-// So waves x u_max <= kStaleBudget = C2's 249, and never more than 2
-// workgroups per CU.
-constexpr double kStaleBudget = 250.0;
+// updates the others do not see yet.  What blows up is a hot syn1neg row
+// taking many stale NEGATIVE updates at once after the reference's sawtooth
+// sets alpha back to 0.025 on an already trained model; the row's share of
+// negative draws per example is u_max = K * max_r p_neg(r) (p_neg: the
+// unigram^0.75 table).  Measured on MI355X:
+//   C2 (V 24,447 Zipf, K 5, u 0.105): 512 workgroups (2,048 waves, waves x u
+//     = 215) track the oracle through the 10-iteration schedule; 768 (323)
+//     diverge in iteration 3; sample = 0 (same u) is stable at 512 too;
+//   C4 (V 60,000, D 512, K 15, u 0.250): 512 (512) diverge in the second
+//     epoch of a 10 M-pair corpus, 242-256 (<= 256) and 128 match the CPU
+//     oracle.
+// So waves x u_max <= kStaleBudget, never more than 2 workgroups per CU.
+constexpr double kStaleBudget = 240.0;
 
 static int default_grid(int cus, int K, int nv, double u_max) {
   int g = std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
@@ -543,20 +542,14 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
     REQUIRE(counts[i] > 0, G2V_EINVAL, "counts[%d] = %lld must be > 0", i, (long long)counts[i]);
   {
     // staleness budget of the Hogwild grid (default_grid)
-    double tot = 0.0, zn = 0.0, zt = 0.0;
-    for (int32_t i = 0; i < c->V; ++i) tot += (double)counts[i];
-    const double thr = sample == 0.0 ? 0.0 : (sample < 1.0 ? sample * tot : sample * 2.618);
-    std::vector<double> pt((size_t)c->V), pn((size_t)c->V);
+    double zn = 0.0;
+    std::vector<double> pn((size_t)c->V);
     for (int32_t i = 0; i < c->V; ++i) {
-      const double v = (double)counts[i];
-      const double keep = thr > 0.0 ? std::min(1.0, (sqrt(v / thr) + 1.0) * (thr / v)) : 1.0;
-      pt[i] = v * keep;
-      pn[i] = pow(v, ns_exponent);
-      zt += pt[i];
+      pn[i] = pow((double)counts[i], ns_exponent);
       zn += pn[i];
     }
     double um = 0.0;
-    for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn + pt[i] / zt);
+    for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn);
     c->u_max = um;
     if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
   }

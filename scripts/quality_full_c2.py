@@ -6,6 +6,7 @@ same job seeds.  Prints the held-in SGNS objective after every iteration and
 one JSON summary line.
 
     python scripts/quality_full_c2.py [--pairs 100000000] [--iters 10] [--threads 16]
+    python scripts/quality_full_c2.py --vocab 60000 --dim 512 --negative 15 --pairs 20000000  # C4
 """
 import argparse
 import json
@@ -31,8 +32,13 @@ def main():
     p.add_argument("--pairs", type=int, default=100_000_000)
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--threads", type=int, default=16)
+    p.add_argument("--vocab", type=int, default=24447)
+    p.add_argument("--dim", type=int, default=200)
+    p.add_argument("--negative", type=int, default=5)
+    p.add_argument("--sample", type=float, default=1e-3)
+    p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
     a = p.parse_args()
-    V0, D, K, sample = 24447, 200, 5, 1e-3
+    V0, D, K, sample = a.vocab, a.dim, a.negative, a.sample
     n = a.pairs
     pairs = S.zipf_gene_pairs(n, V0, 1.0, seed=20250114)
     flat = pairs.reshape(-1)
@@ -60,6 +66,8 @@ def main():
         return float(O.sgns_loss(s0, s1, ec, ej, negs))
 
     eng = E.SGNSEngine(V, D, K)
+    if a.grid:
+        eng.set_option(N.OPT_GRID, a.grid)
     eng.set_vocab(vc, sample)
     eng.set_weights(syn0, np.zeros((V, D), np.float32))
     eng.set_corpus(tok, sent_len=2)
@@ -76,12 +84,13 @@ def main():
         g0, g1 = eng.get_weights()
         t = time.time()
         CO.train(tok, off, js, al.astype(np.float32), E.job_seeds(rs_c, len(js) - 1), si, True,
-                 cum, c0, c1, np.ones(V, np.float32), K, nthreads=a.threads)
+                 cum, c0, c1, np.ones(V, np.float32), K, nthreads=a.threads, ld=(D + 15) // 16 * 16)
         out["cpu_s"] += time.time() - t
         out["gpu"].append(round(loss(g0, g1), 5))
         out["cpu"].append(round(loss(c0, c1), 5))
         print("iter", it, "gpu", out["gpu"][-1], "cpu hogwild", out["cpu"][-1], flush=True)
-    out.update({"pairs": n, "iters": a.iters, "cpu_threads": a.threads,
+    out.update({"pairs": n, "iters": a.iters, "cpu_threads": a.threads, "vocab": V0, "dim": D,
+                "negative": K, "sample": sample, "grid": eng.get_option(N.OPT_GRID),
                 "rel_gap_final": round((out["gpu"][-1] - out["cpu"][-1]) / out["cpu"][-1], 5)})
     print(json.dumps(out))
 
