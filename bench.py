@@ -173,7 +173,7 @@ def main():
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
     merge_backend = "torch"
-    if world > 1 and a.backend == "nccl":
+    if use_dist and a.backend == "nccl":
         # libg2v's own RCCL communicator: rank 0's unique id over the process group
         box = [eng.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
