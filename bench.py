@@ -338,11 +338,14 @@ def main():
                              f"{n_pairs} pairs, dim {D}, neg {K}, window 1, sample {a.sample:g}, "
                              "1 epoch per step") if world == 1 else
                             (f"C3: synthetic Zipf gene pairs, V={V0}, {n_pairs} pairs per GPU x "
-                             f"{world}, dim {D}, neg {K}, RCCL row-wise replica merge ({a.merge}) "
-                             f"every {avg_every} jobs"),
+                             f"{world}, dim {D}, neg {K}, replica merge ({a.merge}) every "
+                             f"{avg_every} jobs: "
+                             + ("libg2v g2v_average (RCCL over xGMI)" if merge_backend == "rccl"
+                                else "torch.distributed gloo rehearsal, ranks sharing a GPU")),
                 "vocab": V, "pairs_per_gpu": n_pairs, "dim": D, "negative": K,
                 "sample": a.sample, "window": 1,
-                "parallelism": f"dp{world}" + (f" + RCCL all-reduce {a.merge} merge" if world > 1 else "")},
+                "parallelism": f"dp{world}" + (f" + {merge_backend} {a.merge} merge"
+                                               if world > 1 else "")},
             "examples_per_s": round(total_examples / elapsed, 1),
             "effective_examples": total_examples,
             "roofline": roofline, "cpu_baseline": cpu, "quality": quality,
