@@ -33,8 +33,9 @@ def bench_line(log):
 
 def main(out):
     c = {}
-    for i in range(1, 5):
-        c.update(counters(os.path.join(out, f"p{i}")))
+    for i in range(1, 6):
+        if os.path.isdir(os.path.join(out, f"p{i}")):
+            c.update(counters(os.path.join(out, f"p{i}")))
     b = bench_line(os.path.join(out, "p1.log"))
     ex = b["effective_examples"]
     launches = max(1, round(ex / (b["roofline"]["algorithmic_bytes_per_launch"]
@@ -58,6 +59,10 @@ def main(out):
         "algorithmic_bytes_per_example": bpe,
         "traffic_over_algorithmic": (fetch + write) / bpe,
     }
+    for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
+              "SQ_INSTS_LDS"):
+        if k in c:  # wave-instructions per directed example
+            res[k.lower() + "_per_example"] = c[k] / ex
     print(json.dumps(res, indent=1))
 
 
