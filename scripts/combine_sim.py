@@ -4,6 +4,8 @@ pending in the same window of consecutive examples, on the C2 record stream
 (oracle sampler, 2 M pairs) -- DESIGN.md section 5c."""
 import os
 import sys
+
+import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gene2vec_amd import engine as E, synthetic as S
 from oracle import c_oracle as CO
