@@ -173,12 +173,20 @@ def main():
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
     merge_backend = "torch"
+    merge_note = None
     if use_dist and a.backend == "nccl":
         # libg2v's own RCCL communicator: rank 0's unique id over the process group
         box = [eng.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
-        eng.comm_init(box[0], world, rank)
-        merge_backend = "rccl"
+        try:
+            eng.comm_init(box[0], world, rank)
+            merge_backend = "rccl"
+        except N.G2VError as e:  # keep the run measurable: torch merges the bound tables
+            merge_note = f"g2v_comm_init failed ({e}); torch.distributed merge used"
+        ok = torch.tensor([1 if merge_backend == "rccl" else 0], device=dev)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if ok.item() == 0:  # every rank must merge the same way
+            merge_backend = "torch"
     trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=a.merge,
                                 backend=merge_backend)
     torch.cuda.synchronize(dev)
@@ -349,6 +357,8 @@ def main():
             "examples_per_s": round(total_examples / elapsed, 1),
             "effective_examples": total_examples,
             "roofline": roofline, "cpu_baseline": cpu, "quality": quality,
+            "merge": ({"backend": merge_backend, "rule": a.merge, "every_jobs": avg_every,
+                       "merges": trainer.averages, "note": merge_note} if world > 1 else None),
             "gpu_event_ms": round(gpu_ms, 3), "wall_s": round(wall, 4),
             "corpus_gen_s": round(t_corpus, 2),
         }
