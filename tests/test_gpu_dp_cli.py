@@ -4,8 +4,8 @@ pairs and merges the replicas row-wise over the process group (the
 reference itself is one process, src/gene2vec.py:59).  The round's box has one
 GPU, so two ranks share cuda:0 over gloo here; the 8-GPU node runs the same code
 over RCCL.  Checks: rank 0 alone writes the outputs every rank reloads, and the
-model's held-in SGNS objective improves at least 85 % as much as the
-single-process run's."""
+model's held-in SGNS objective improves at least 93 % as much as the
+single-process run's (measured 97 %)."""
 import os
 import socket
 import subprocess
@@ -78,5 +78,6 @@ def test_cli_data_parallel_two_ranks(tmp_path):
     assert l1 < 0.9 * init and l2 < 0.9 * init
     # model averaging halves the step of rows both replicas train between merges
     # (distributed.touch_merge_): the replicas learn a little slower than one
-    # process on a corpus this small; bar: 85 % of the single run's improvement
-    assert (init - l2) >= 0.85 * (init - l1), (l1, l2)
+    # process on a corpus this small; bar: 93 % of the single run's improvement
+    # (measured 2.8221 vs 2.7867 = 97 %)
+    assert (init - l2) >= 0.93 * (init - l1), (l1, l2)
