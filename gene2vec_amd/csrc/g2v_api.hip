@@ -15,7 +15,6 @@
 #include <algorithm>
 #include <mutex>
 #include <new>
-#include <queue>
 #include <thread>
 #include <string>
 #include <utility>
@@ -171,24 +170,6 @@ struct g2v_ctx {
   bool merge_valid = false;
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
-
-  // owned syn0 rows (k_sgns_atomic<..., OWN>): input-row share of each row
-  // (downsampled token distribution, from set_vocab), the owner map for the
-  // current grid, and the bucketing workspace
-  int owned = 1;  // G2V_OPT_OWNED_ROWS
-  std::vector<double> p_tok;
-  int own_grid = 0, own_cap = 0, own_stripe_rows = -1;
-  int32_t* d_own_code = nullptr;   // [V]
-  int32_t* d_own_rows = nullptr;   // [grid][cap]
-  int64_t own_rows_cap = 0;
-  int32_t* d_rec_q = nullptr;      // records in queue order
-  int64_t rec_q_cap = 0;
-  int32_t* d_blk_cnt = nullptr;
-  int64_t* d_blk_off = nullptr;
-  int64_t* d_q_tot = nullptr;
-  int64_t* d_qoff = nullptr;
-  int64_t blk_cap = 0, blk_off_cap = 0, q_cap = 0, qoff_cap = 0;
-  int64_t seg_max_ex = 0;          // bound on the current segment's records
   int64_t jobs = 0, launches = 0;
 
   // timing
@@ -452,13 +433,6 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->merge0);
   dev_free(c->merge1);
   dev_free(c->merge_cnt);
-  dev_free(c->d_own_code);
-  dev_free(c->d_own_rows);
-  dev_free(c->d_rec_q);
-  dev_free(c->d_blk_cnt);
-  dev_free(c->d_blk_off);
-  dev_free(c->d_q_tot);
-  dev_free(c->d_qoff);
   comm_destroy(c);
   dev_free(c->stripe);
   dev_free(c->dbg16);
@@ -524,12 +498,8 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value >= 1 && value <= 16, G2V_EINVAL, "stripe copies out of [1, 16]");
       c->stripe_copies = (int)value;
       return G2V_OK;
-    case G2V_OPT_OWNED_ROWS:
-      REQUIRE(value == 0 || value == 1, G2V_EINVAL, "owned rows must be 0 or 1");
-      c->owned = (int)value;
-      return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 5, G2V_EINVAL, "debug write mode out of [0, 5]");
+      REQUIRE(value >= 0 && value <= 4, G2V_EINVAL, "debug write mode out of [0, 4]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_GRID:
@@ -552,7 +522,6 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_DEBUG_WRITE: *out = c->debug_write; return G2V_OK;
     case G2V_OPT_STRIPE_ROWS: *out = c->stripe_rows; return G2V_OK;
     case G2V_OPT_STRIPE_COPIES: *out = c->stripe_copies; return G2V_OK;
-    case G2V_OPT_OWNED_ROWS: *out = c->owned; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -582,19 +551,6 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
     double um = 0.0;
     for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn);
     c->u_max = um;
-    // expected input-row share (downsampled tokens) for the owned-row map
-    double tot = 0.0, zt = 0.0;
-    for (int32_t i = 0; i < c->V; ++i) tot += (double)counts[i];
-    const double thr = sample == 0.0 ? 0.0 : (sample < 1.0 ? sample * tot : sample * 2.618);
-    c->p_tok.assign((size_t)c->V, 0.0);
-    for (int32_t i = 0; i < c->V; ++i) {
-      const double v = (double)counts[i];
-      const double keep = thr > 0.0 ? std::min(1.0, (sqrt(v / thr) + 1.0) * (thr / v)) : 1.0;
-      c->p_tok[i] = v * keep;
-      zt += c->p_tok[i];
-    }
-    for (auto& x : c->p_tok) x /= zt;
-    c->own_grid = 0;  // owner map rebuilt at the next train
     if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
   }
   HIPCHK(hipMemcpyAsync(c->d_counts, counts, sizeof(int64_t) * c->V, hipMemcpyHostToDevice,
@@ -828,7 +784,6 @@ static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing) {
   const int64_t tk = tokens_between(c, hjs[j0], hjs[j0 + nj]);
   if (tk >= 0) max_ex = std::max<int64_t>(2 * std::min<int64_t>(tk, nj * (int64_t)kBatchWords), 1);
   if ((rc = dev_reserve(c->stream, &c->d_rec, &c->rec_cap, max_ex * c->rec_stride))) return rc;
-  c->seg_max_ex = max_ex;
 
   SampleArgs a{};
   a.tok = c->tok;
@@ -865,98 +820,10 @@ static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing) {
   return G2V_OK;
 }
 
-// ---------------------------------------------------------------------------
-// owned syn0 rows (G2V_OPT_OWNED_ROWS): which workgroup owns which input row
-// ---------------------------------------------------------------------------
-// LDS row slots per workgroup: <= 64 KB of dynamic LDS beside the kernel's
-// ~12-16 KB static LDS keeps two 256-thread workgroups per CU (160 KB)
-static int own_capacity(int nvec) { return std::min(255, 65536 / (nvec * 16)); }
-
-static bool owned_applies(const g2v_ctx* c, int mode) {
-  return c->owned && mode == kModeHogwild && c->nv == 1 && c->debug_write == 0 &&
-         (c->hot_rows < 0 || c->hot_rows >= c->V) && c->sgns_grid >= 1 &&
-         c->sgns_grid <= kMaxQueues && (int64_t)c->p_tok.size() == c->V;
-}
-
-// Longest-processing-time assignment of the input rows, in descending share,
-// each to the least-loaded workgroup with a free LDS slot.  A row whose
-// expected share of the examples exceeds one workgroup's (1/grid), and the
-// striped rows, stay shared: their examples are dealt round-robin over the
-// queues, so every queue carries the same shared load on top of its owned one.
-static int build_owner_map(g2v_ctx* c) {
-  const int G = c->sgns_grid;
-  const int stripe = c->stripe_copies > 1 ? std::min(c->stripe_rows, c->V) : 0;
-  if (c->own_grid == G && c->own_stripe_rows == stripe && c->d_own_code) return G2V_OK;
-  const int cap = own_capacity(c->nvec);
-  const double fill = 0.95 / G;
-  std::vector<int32_t> code((size_t)c->V, -1), rows((size_t)G * cap, -1);
-  std::vector<int> nrows((size_t)G, 0);
-  typedef std::pair<double, int> Load;
-  std::priority_queue<Load, std::vector<Load>, std::greater<Load>> heap;
-  for (int q = 0; q < G; ++q) heap.push(Load(0.0, q));
-  for (int32_t r = 0; r < c->V && !heap.empty(); ++r) {
-    if (r < stripe || c->p_tok[r] > fill) continue;
-    const Load top = heap.top();
-    heap.pop();
-    const int q = top.second;
-    code[r] = q * 256 + nrows[q];
-    rows[(size_t)q * cap + nrows[q]] = r;
-    if (++nrows[q] < cap) heap.push(Load(top.first + c->p_tok[r], q));
-  }
-  int rc;
-  HIPCHK(hipStreamSynchronize(c->stream));  // the previous map may be in use
-  if (!c->d_own_code && (rc = dev_alloc(&c->d_own_code, (size_t)c->V))) return rc;
-  if ((rc = dev_reserve(c->stream, &c->d_own_rows, &c->own_rows_cap, (int64_t)G * cap))) return rc;
-  HIPCHK(hipMemcpy(c->d_own_code, code.data(), sizeof(int32_t) * c->V, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(c->d_own_rows, rows.data(), sizeof(int32_t) * rows.size(),
-                   hipMemcpyHostToDevice));
-  c->own_grid = G;
-  c->own_cap = cap;
-  c->own_stripe_rows = stripe;
-  return G2V_OK;
-}
-
-// the segment's records (gensim order, d_rec) -> one queue per workgroup (d_rec_q)
-static int bucket_segment(g2v_ctx* c, const int64_t* n_examples_dev, bool timing) {
-  const int G = c->own_grid;
-  const int64_t nblk = (c->seg_max_ex + kBucketRecs - 1) / kBucketRecs;
-  int rc;
-  if ((rc = dev_reserve(c->stream, &c->d_rec_q, &c->rec_q_cap, c->seg_max_ex * c->rec_stride)))
-    return rc;
-  if ((rc = dev_reserve(c->stream, &c->d_blk_cnt, &c->blk_cap, nblk * G)) ||
-      (rc = dev_reserve(c->stream, &c->d_blk_off, &c->blk_off_cap, nblk * G)) ||
-      (rc = dev_reserve(c->stream, &c->d_q_tot, &c->q_cap, (int64_t)G)) ||
-      (rc = dev_reserve(c->stream, &c->d_qoff, &c->qoff_cap, (int64_t)G + 1)))
-    return rc;
-  BucketArgs b{};
-  b.rec = c->d_rec;
-  b.out = c->d_rec_q;
-  b.rec_stride = c->rec_stride;
-  b.n_examples = n_examples_dev;
-  b.max_examples = c->seg_max_ex;
-  b.own_code = c->d_own_code;
-  b.nq = G;
-  b.blk_cnt = c->d_blk_cnt;
-  b.blk_off = c->d_blk_off;
-  b.q_tot = c->d_q_tot;
-  b.qoff = c->d_qoff;
-  hipEvent_t e0 = nullptr, e1 = nullptr;
-  if (timing) {
-    if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
-    HIPCHK(hipEventRecord(e0, c->stream));
-  }
-  HIPCHK(launch_bucket_records(b, c->stream));
-  if (timing) {
-    HIPCHK(hipEventRecord(e1, c->stream));
-    c->t_samp.emplace_back(e0, e1);
-  }
-  return G2V_OK;
-}
-
 static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool timing,
-                    bool closs, const float* rd0, const float* rd1, bool owned = false) {
+                    bool closs, const float* rd0, const float* rd1) {
   SgnsArgs s{};
-  s.rec = owned ? c->d_rec_q : c->d_rec;
+  s.rec = c->d_rec;
   s.rec_stride = c->rec_stride;
   s.n_examples = n_examples_dev;
   s.rd0 = rd0;
@@ -995,21 +862,12 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
   }
   s.dbg16 = c->dbg16;
-  if (owned) {
-    s.own_code = c->d_own_code;
-    s.own_rows = c->d_own_rows;
-    s.qoff = c->d_qoff;
-    s.own_cap = c->own_cap;
-  }
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timing) {
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
     HIPCHK(hipEventRecord(e0, c->stream));
   }
-  if (owned)
-    HIPCHK(launch_sgns_owned(s, c->K, c->own_grid, (size_t)c->own_cap * c->nvec * 16, c->stream));
-  else
-    HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
+  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
   HIPCHK(launch_fold_stripes(c->syn0, c->syn1, c->stripe, s.stripe_rows, s.stripe_copies, c->ld,
                              c->nvec, c->stream));
   if (timing) {
@@ -1091,14 +949,10 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
   const bool timing = flags & G2V_FLAG_TIMING;
   const bool closs = flags & G2V_FLAG_COMPUTE_LOSS;
   if ((rc = upload_jobs(c, job_sent, job_alpha, job_seed, n_jobs))) return rc;
-  const bool owned = owned_applies(c, mode);
-  if (owned && (rc = build_owner_map(c))) return rc;
   for (int64_t j0 = 0; j0 < n_jobs; j0 += c->seg_jobs) {
     const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
     if ((rc = sample_segment(c, j0, nj, timing))) return rc;
-    if (owned && (rc = bucket_segment(c, c->d_job_exoff + nj, timing))) return rc;
-    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, closs, c->syn0, c->syn1, owned)))
-      return rc;
+    if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, closs, c->syn0, c->syn1))) return rc;
   }
   c->jobs += n_jobs;
   return G2V_OK;

@@ -95,37 +95,7 @@ struct SgnsArgs {
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])
   float* loss_f32;          // sequential: gensim's float32 running sum, continued
   double* loss_f64;         // parallel modes: per-wave float partials summed in double
-  // owned syn0 rows (k_sgns_atomic<..., OWN>): workgroup b trains the records
-  // of queue b = [qoff[b], qoff[b+1]); the syn0 rows it owns live in its LDS
-  // for the whole launch (reads from LDS, updates as LDS atomics, written back
-  // at the end), every other input row is shared (global atomics)
-  const int32_t* own_code;  // [V] owner * 256 + LDS slot, -1 = shared
-  const int32_t* own_rows;  // [grid][own_cap] vocabulary row of each slot, -1 = empty
-  const int64_t* qoff;      // [grid + 1] queue offsets into rec
-  int own_cap;              // LDS row slots per workgroup
 };
-
-// owned-row bucketing of a segment's records (g2v_kernels.hip): records are
-// counted per (block of kBucketRecs records, queue), the counts scanned
-// queue-major, and the records scattered so queue b holds, in record order
-// block by block, the records whose input row workgroup b owns plus every
-// grid-th shared record
-constexpr int kBucketRecs = 4096;
-constexpr int kMaxQueues = 1024;
-struct BucketArgs {
-  const int32_t* rec;       // [E][rec_stride], gensim order
-  int32_t* out;             // [E][rec_stride], queue order
-  int rec_stride;
-  const int64_t* n_examples;  // device scalar E
-  int64_t max_examples;     // host bound on E (grid sizing)
-  const int32_t* own_code;  // [V]
-  int nq;                   // queues (= SGNS workgroups)
-  int32_t* blk_cnt;         // [nblk][nq]
-  int64_t* blk_off;         // [nblk][nq] -> queue-local offsets
-  int64_t* q_tot;           // [nq]
-  int64_t* qoff;            // [nq + 1]
-};
-hipError_t launch_bucket_records(const BucketArgs& a, hipStream_t st);
 
 hipError_t launch_job_sample(bool write, const SampleArgs& a, int64_t n_jobs, hipStream_t st);
 hipError_t launch_scan_jobs(const int32_t* nex, int64_t nj, int64_t* off,
@@ -143,16 +113,12 @@ hipError_t launch_explicit_records(const int32_t* center, const int32_t* input,
   hipError_t launch_sgns_k##KK(const SgnsArgs& a, int nv, int mode, int pol, int grid,     \
                                hipStream_t st);                                            \
   hipError_t launch_sgns_atomic_k##KK(const SgnsArgs& a, int nv, int grid, hipStream_t st); \
-  hipError_t launch_sgns_owned_k##KK(const SgnsArgs& a, int grid, size_t lds_bytes,            \
-                                     hipStream_t st);                                          \
   int sgns_blocks_per_cu_k##KK(int nv);
 G2V_FOR_EACH_K(G2V_DECL_K)
 bool sgns_supported(int K, int nv);
 hipError_t launch_sgns(const SgnsArgs& a, int K, int nv, int mode, int pol, int grid,
                        hipStream_t st);
 hipError_t launch_sgns_atomic(const SgnsArgs& a, int K, int nv, int grid, hipStream_t st);
-hipError_t launch_sgns_owned(const SgnsArgs& a, int K, int grid, size_t lds_bytes,
-                             hipStream_t st);
 int sgns_blocks_per_cu(int K, int nv);
 hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
                                int64_t ld, int nvec, hipStream_t st);

@@ -354,100 +354,6 @@ hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
 }
 
 // ---------------------------------------------------------------------------
-// owned-row bucketing (k_sgns_atomic<..., OWN>): queue of a record = the
-// workgroup that owns its input row, or record index % nq for a shared row
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ int rec_queue(const BucketArgs& a, int64_t i) {
-  const int32_t input = a.rec[i * a.rec_stride + 1];
-  const int32_t code = a.own_code[input];
-  return code >= 0 ? (code >> 8) : (int)(i % a.nq);
-}
-
-// records [b*kBucketRecs, ...) of block b: per-queue counts
-__global__ __launch_bounds__(256) void k_bucket_count(BucketArgs a) {
-  __shared__ int s_cnt[kMaxQueues];
-  const int64_t E = *a.n_examples;
-  const int64_t b0 = (int64_t)blockIdx.x * kBucketRecs;
-  for (int q = threadIdx.x; q < a.nq; q += 256) s_cnt[q] = 0;
-  __syncthreads();
-  const int64_t b1 = b0 + kBucketRecs < E ? b0 + kBucketRecs : E;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += 256) atomicAdd(&s_cnt[rec_queue(a, i)], 1);
-  __syncthreads();
-  for (int q = threadIdx.x; q < a.nq; q += 256)
-    a.blk_cnt[(int64_t)blockIdx.x * a.nq + q] = s_cnt[q];
-}
-
-// one block per queue: exclusive scan of its counts over the record blocks
-__global__ __launch_bounds__(1024) void k_bucket_scan_q(BucketArgs a, int64_t nblk) {
-  __shared__ int s_scan[16];
-  const int q = blockIdx.x;
-  int64_t carry = 0;
-  for (int64_t b0 = 0; b0 < nblk; b0 += 1024) {
-    const int64_t b = b0 + threadIdx.x;
-    const int v = b < nblk ? a.blk_cnt[b * a.nq + q] : 0;
-    int tot;
-    const int ex = block_excl_scan<1024>(v, s_scan, tot);
-    if (b < nblk) a.blk_off[b * a.nq + q] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) a.q_tot[q] = carry;
-}
-
-// queue starts (one block)
-__global__ __launch_bounds__(1024) void k_bucket_scan_tot(BucketArgs a) {
-  __shared__ int s_scan[16];
-  int64_t carry = 0;
-  for (int q0 = 0; q0 < a.nq; q0 += 1024) {
-    const int q = q0 + threadIdx.x;
-    const int v = q < a.nq ? (int)a.q_tot[q] : 0;
-    int tot;
-    const int ex = block_excl_scan<1024>(v, s_scan, tot);
-    if (q < a.nq) a.qoff[q] = carry + ex;
-    carry += tot;
-  }
-  if (threadIdx.x == 0) a.qoff[a.nq] = carry;
-}
-
-// scatter: queue q's records keep block order; inside a block of 4,096
-// records their order follows the LDS counter
-__global__ __launch_bounds__(256) void k_bucket_scatter(BucketArgs a) {
-  __shared__ unsigned long long s_pos[kMaxQueues];
-  const int64_t E = *a.n_examples;
-  const int64_t b0 = (int64_t)blockIdx.x * kBucketRecs;
-  for (int q = threadIdx.x; q < a.nq; q += 256)
-    s_pos[q] = (unsigned long long)(a.qoff[q] + a.blk_off[(int64_t)blockIdx.x * a.nq + q]);
-  __syncthreads();
-  const int64_t b1 = b0 + kBucketRecs < E ? b0 + kBucketRecs : E;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += 256) {
-    const int q = rec_queue(a, i);
-    const int64_t pos = (int64_t)atomicAdd(&s_pos[q], 1ull);
-    const int4* src = reinterpret_cast<const int4*>(a.rec + i * a.rec_stride);
-    int4* dst = reinterpret_cast<int4*>(a.out + pos * a.rec_stride);
-    for (int w = 0; w < a.rec_stride / 4; ++w) dst[w] = src[w];
-  }
-}
-
-hipError_t launch_bucket_records(const BucketArgs& a, hipStream_t st) {
-  const int64_t nblk = (a.max_examples + kBucketRecs - 1) / kBucketRecs;
-  if (nblk <= 0 || a.nq <= 0 || a.nq > kMaxQueues) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)nblk), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(k_bucket_scan_q, dim3((unsigned)a.nq), dim3(1024), 0, st, a, nblk);
-  hipLaunchKernelGGL(k_bucket_scan_tot, dim3(1), dim3(1024), 0, st, a);
-  hipLaunchKernelGGL(k_bucket_scatter, dim3((unsigned)nblk), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t launch_sgns_owned(const SgnsArgs& a, int K, int grid, size_t lds_bytes,
-                             hipStream_t st) {
-  switch (K) {
-#define G2V_CASE(KK) case KK: return launch_sgns_owned_k##KK(a, grid, lds_bytes, st);
-    G2V_FOR_EACH_K(G2V_CASE)
-#undef G2V_CASE
-    default: return hipErrorInvalidValue;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // replica merge (g2v_average / g2v_average_local): one wave per row, lane l
 // owns float4 columns l, l+64; HBM-bound streaming (rows are 128-B aligned)
 // ---------------------------------------------------------------------------

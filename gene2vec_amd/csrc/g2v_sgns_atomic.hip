@@ -28,7 +28,6 @@ template <int K, int NV>
 struct ExRegs {
   int32_t tg[K + 1];
   int32_t input;
-  int32_t slot;  // OWN: LDS slot of the input row when this workgroup owns it, else -1
   float alpha;
   float4 l1[NV];
   float4 rw[K + 1][NV];
@@ -76,7 +75,7 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
   return a.stripe + (((int64_t)tbl * (a.stripe_copies - 1) + (c - 1)) * a.stripe_rows + t) * a.ld;
 }
 
-template <int K, int NV, bool OWN = false>
+template <int K, int NV>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a, int64_t e,
                                              __amdgpu_buffer_rsrc_t r0,
                                              __amdgpu_buffer_rsrc_t r1, int rowb, int lane,
@@ -87,13 +86,7 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
 #pragma unroll
   for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
-  x.slot = -1;
-  if (OWN) {
-    const int32_t code = __builtin_amdgcn_readfirstlane(a.own_code[x.input]);
-    if (code >= 0 && (code >> 8) == (int)blockIdx.x) x.slot = code & 255;
-  }
-  // an owned input row is read from LDS when the example is computed
-  if (x.slot < 0) load_row<NV>(x.l1, a, r0, x.input, 0, rowb, lane, on);
+  load_row<NV>(x.l1, a, r0, x.input, 0, rowb, lane, on);
 #pragma unroll
   for (int d = 0; d <= K; ++d) {
     if (x.tg[d] >= 0) {
@@ -108,52 +101,27 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
 // 2 no table writes, 3 packed-f16 atomics into a scratch table (half the atomic
 // bytes, tables never written: a throughput probe), 4 the production f32
-// atomics into that scratch table (tables never written), 5 production
-// without the syn0 updates (the bound of any scheme that takes syn0 off the
-// atomic path)
+// atomics into that scratch table (tables never written)
 template <int WR>
 __device__ __forceinline__ void upd(float* p, float v) {
-  if (WR == 0 || WR == 4 || WR == 5) atomicAdd(p, v);
+  if (WR == 0 || WR == 4) atomicAdd(p, v);
   else if (WR == 1) *p = v;
 }
 
 // LOSS ([ext] compute_loss): each wave keeps a float32 partial of the
 // -log(sigmoid(+-f)) LOG_TABLE terms over its chunk and adds it to a double
 // accumulator once per chunk; LOSS = false compiles the tally out.
-//
-// OWN (owned syn0 rows; NV = 1): the segment's records arrive bucketed into one
-// queue per workgroup (launch_bucket_records): queue b holds the examples
-// whose input row workgroup b owns, in record order, plus every grid-th
-// example of a shared (hot) input row.  The owned syn0 rows stay in this
-// workgroup's LDS for the whole launch: an example reads its input row from
-// LDS when it is computed (after this wave's previous LDS adds, so a wave
-// always sees its own updates) and adds lockf*work back with LDS float
-// atomics (ds_add_f32: no update is lost between the 4 waves, none goes to the
-// memory-side atomic unit); the rows are written back at the end.  No other
-// workgroup reads or writes an owned row during the launch.  Shared rows take
-// the global path (atomics, stripes) as in the plain kernel.
-template <int K, int NV, int WR = 0, bool LOSS = false, bool OWN = false>
+template <int K, int NV, int WR = 0, bool LOSS = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
-  static_assert(!OWN || NV == 1, "owned rows: one float4 column per lane");
   __shared__ float s_lut[kExpTableSize];
   __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
   __shared__ float s_wk[W][256 * NV];
-  extern __shared__ float4 s_own[];  // OWN: [own_cap][nvec]
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
     s_lut[i] = a.exp_table[i];
     if (LOSS) s_log[i] = a.log_table[i];
-  }
-  const int32_t* own_rows = OWN ? a.own_rows + (int64_t)blockIdx.x * a.own_cap : nullptr;
-  if (OWN) {
-    for (int i = threadIdx.x; i < a.own_cap * a.nvec; i += kSgnsThreads) {
-      const int slot = i / a.nvec, col = i - slot * a.nvec;
-      const int32_t r = own_rows[slot];
-      s_own[i] = r >= 0 ? reinterpret_cast<const float4*>(a.rd0 + (int64_t)r * a.ld)[col]
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
   }
   __syncthreads();
 
@@ -176,22 +144,14 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
   for (int v = 0; v < NV; ++v) on[v] = (lane + 64 * v) < a.nvec;
 
-  // plain: chunks of the whole segment over all waves; OWN: chunks of this
-  // workgroup's queue over its waves
-  const int64_t q_beg = OWN ? a.qoff[blockIdx.x] : 0;
-  const int64_t q_end = OWN ? a.qoff[blockIdx.x + 1] : E;
-  const int64_t c_first = OWN ? (int64_t)wid : gw;
-  const int64_t c_step = OWN ? (int64_t)W : nw;
-  for (int64_t c = c_first; q_beg + c * kChunk < q_end; c += c_step) {
-    const int64_t e_beg = q_beg + c * kChunk;
-    const int64_t e_end = (e_beg + kChunk < q_end) ? e_beg + kChunk : q_end;
+  for (int64_t c = gw; c * kChunk < E; c += nw) {
+    const int64_t e_beg = c * kChunk;
+    const int64_t e_end = (e_beg + kChunk < E) ? e_beg + kChunk : E;
     float lsum = 0.f;
     ExRegs<K, NV> x;
-    load_example<K, NV, OWN>(x, a, e_beg, r0, r1, rowb, lane, on);
+    load_example<K, NV>(x, a, e_beg, r0, r1, rowb, lane, on);
     for (int64_t e = e_beg; e < e_end; ++e) {
       // ---- compute example e ------------------------------------------------
-      if (OWN && x.slot >= 0)
-        x.l1[0] = on[0] ? s_own[x.slot * a.nvec + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
       double pd[NT], dot[NT];
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
@@ -263,20 +223,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int d = 0; d < NT; ++d) tg[d] = x.tg[d];
       const int32_t input = x.input;
-      const int32_t slot = x.slot;
       const float lf = any ? a.lockf[input] : 0.f;
-      if (OWN && slot >= 0 && any && on[0]) {
-        // owned syn0 row: LDS float atomics, no memory-side traffic
-        float* p = reinterpret_cast<float*>(s_own + slot * a.nvec + lane);
-        atomicAdd(p + 0, lf * work[0].x);
-        atomicAdd(p + 1, lf * work[0].y);
-        atomicAdd(p + 2, lf * work[0].z);
-        atomicAdd(p + 3, lf * work[0].w);
-      }
-      const bool glob0 = !OWN || slot < 0;  // syn0 row takes the global path
 
       // ---- prefetch example e+1 (its loads overtake e's atomics) -------------
-      if (e + 1 < e_end) load_example<K, NV, OWN>(x, a, e + 1, r0, r1, rowb, lane, on);
+      if (e + 1 < e_end) load_example<K, NV>(x, a, e + 1, r0, r1, rowb, lane, on);
 
       // ---- atomics of example e -----------------------------------------------
       const int cbase = (int)(e % (int64_t)a.stripe_copies);
@@ -313,7 +263,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         float* row = upd_row<WR>(a, 1, tg[d], (cbase + d) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, g[d] * s1[64 * i + lane]);
       }
-      if (any && WR != 5 && glob0) {
+      if (any) {
         float* row = upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, lf * sw[64 * i + lane]);
       }
@@ -332,8 +282,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
             }
           }
           const bool from_work = (q == NT);
-          if (from_work && (WR == 5 || !glob0)) coef = 0.f;  // skipped / owned (LDS)
-          if (from_work && WR != 5 && glob0) {
+          if (from_work) {
             coef = any ? lf : 0.f;
             row_t = input;
           }
@@ -347,15 +296,6 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       __builtin_amdgcn_wave_barrier();
     }
     if (LOSS && lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);
-  }
-  if (OWN) {
-    // every wave's LDS adds are done: write the owned rows back
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.own_cap * a.nvec; i += kSgnsThreads) {
-      const int slot = i / a.nvec, col = i - slot * a.nvec;
-      const int32_t r = own_rows[slot];
-      if (r >= 0) reinterpret_cast<float4*>(a.wr0 + (int64_t)r * a.ld)[col] = s_own[i];
-    }
   }
 }
 
@@ -376,10 +316,6 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 2) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
-    return hipGetLastError();
-  }
-  if (nv == 1 && a.debug_write == 5) {
-    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 5>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
   if (nv == 1 && a.debug_write == 4) {
@@ -404,17 +340,6 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
     hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
   else
     hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
-  return hipGetLastError();
-}
-
-hipError_t G2V_CAT(launch_sgns_owned_k, G2V_K)(const SgnsArgs& a, int grid, size_t lds_bytes,
-                                                hipStream_t st) {
-  if (a.compute_loss)
-    hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true, true>), dim3(grid), dim3(kSgnsThreads),
-                       lds_bytes, st, a);
-  else
-    hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, false, true>), dim3(grid), dim3(kSgnsThreads),
-                       lds_bytes, st, a);
   return hipGetLastError();
 }
 

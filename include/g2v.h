@@ -116,12 +116,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         atomics into a scratch table [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off [8] (values stay exact:
- *                         readers sum the copies, each launch folds them back)
- *   G2V_OPT_OWNED_ROWS    HOGWILD g2v_train, D <= 256: each workgroup owns the syn0
- *                         rows of a share of the vocabulary for a launch (kept in
- *                         its LDS, updated with LDS atomics; the segment's
- *                         examples bucketed by owner, record order kept per
- *                         owner); hot rows stay shared [1] */
+ *                         readers sum the copies, each launch folds them back) */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
@@ -130,7 +125,6 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_DEBUG_WRITE 6
 #define G2V_OPT_STRIPE_ROWS 7
 #define G2V_OPT_STRIPE_COPIES 8
-#define G2V_OPT_OWNED_ROWS 9
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest

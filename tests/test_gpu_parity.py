@@ -518,43 +518,3 @@ def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s):
     l_gpu = _eval_loss(g0, g1, tok, counts, K)
     l_ref = _eval_loss(a0, a1, tok, counts, K)
     assert abs(l_gpu - l_ref) / l_ref < 0.005, (V, zipf_s, grid, l_gpu, l_ref)
-
-
-@pytest.mark.parametrize("V,sample", [(24447, 1e-3), (3000, 0.0)])
-def test_owned_rows_track_shared_kernel_and_oracle(V, sample):
-    """G2V_OPT_OWNED_ROWS (default on for D <= 256): each workgroup keeps the
-    syn0 rows it owns in LDS for the launch.  Same data, same seeds: the held-in
-    objective with owned rows equals the plain kernel's and the sequential
-    oracle's within 0.3 % after 2 gensim iterations."""
-    D, K = 200, 5
-    tok, counts, syn0 = _zipf_setup(1_000_000, V, D, K, sample, seed=41)
-    V = len(counts)
-    n = len(tok) // 2
-    off = np.arange(0, len(tok) + 1, 2, dtype=np.int64)
-    js = E.plan_jobs(n_sent=n, sent_len=2)
-    res = {}
-    for owned in (1, 0):
-        eng = E.SGNSEngine(V, D, K)
-        eng.set_option(N.OPT_OWNED_ROWS, owned)
-        assert eng.get_option(N.OPT_OWNED_ROWS) == owned
-        eng.set_vocab(counts, sample)
-        eng.set_weights(syn0, np.zeros((V, D), np.float32))
-        eng.set_corpus(tok, sent_len=2)
-        rs = np.random.RandomState(1)
-        for _ in range(2):
-            eng.train(js, E.job_alphas(js, n), E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)
-        st = eng.read_stats()
-        g0, g1 = eng.get_weights()
-        eng.close()
-        assert np.isfinite(g0).all() and np.isfinite(g1).all()
-        res[owned] = (_eval_loss(g0, g1, tok, counts, K), st["examples"])
-    a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
-    rs = np.random.RandomState(1)
-    for _ in range(2):
-        CO.train(tok, off, js, E.job_alphas(js, n).astype(np.float32), E.job_seeds(rs, len(js) - 1),
-                 CO.sample_int(counts, sample), sample != 0, CO.make_cum_table(counts), a0, a1,
-                 np.ones(V, np.float32), K)
-    l_ref = _eval_loss(a0, a1, tok, counts, K)
-    assert res[0][1] == res[1][1]  # same examples trained
-    for owned in (1, 0):
-        assert abs(res[owned][0] - l_ref) / l_ref < 0.003, (owned, res, l_ref)
