@@ -101,7 +101,7 @@ struct g2v_ctx {
   int64_t ld = 0;
   int cus = 0, sgns_grid = 0;
   bool grid_user = false;       // G2V_OPT_GRID set explicitly
-  double u_max = 0.0;           // hottest row's negative draws per example (set_vocab)
+  double u_max = 0.0;           // hottest row's updates per example (set_vocab)
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
@@ -179,19 +179,20 @@ struct g2v_ctx {
 };
 
 // Hogwild staleness bound.  Every wave in flight holds one example whose
-// updates the others do not see yet.  What blows up is a hot syn1neg row
-// taking many stale NEGATIVE updates at once after the reference's sawtooth
-// sets alpha back to 0.025 on an already trained model; the row's share of
-// negative draws per example is u_max = K * max_r p_neg(r) (p_neg: the
-// unigram^0.75 table).  Measured on MI355X:
-//   C2 (V 24,447 Zipf, K 5, u 0.105): 512 workgroups (2,048 waves, waves x u
-//     = 215) track the oracle through the 10-iteration schedule; 768 (323)
-//     diverge in iteration 3; sample = 0 (same u) is stable at 512 too;
-//   C4 (V 60,000, D 512, K 15, u 0.250): 512 (512) diverge in the second
-//     epoch of a 10 M-pair corpus, 242-256 (<= 256) and 128 match the CPU
-//     oracle.
+// updates the others do not see yet.  What blows up is a hot row taking many
+// stale updates at once after the reference's sawtooth sets alpha back to
+// 0.025 on an already trained model.  A row's share of the updates per
+// example is u(r) = K * p_neg(r) (syn1neg, unigram^0.75 negatives) + p_tok(r)
+// (its share of kept tokens: syn0 input and syn1neg centre); u_max = max_r.
+// Measured on MI355X (waves x u_max in brackets):
+//   C2 (V 24,447 Zipf, K 5, sample 1e-3, u 0.122): 512 workgroups [249] track
+//     the oracle through the 10-iteration schedule; 768 [374] diverge;
+//   C4 (V 60,000, D 512, K 15, u 0.267): 512 [546] diverge in the second
+//     epoch of a 10 M-pair corpus, 256 [273] and 128 [137] match the oracle;
+//   V 3,000 Zipf, sample 0 (u 0.308): 512 [630] and 318 [391] diverge,
+//     204 [251] and 128 [157] match the sequential oracle.
 // So waves x u_max <= kStaleBudget, never more than 2 workgroups per CU.
-constexpr double kStaleBudget = 240.0;
+constexpr double kStaleBudget = 250.0;
 
 static int default_grid(int cus, int K, int nv, double u_max) {
   int g = std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
@@ -499,7 +500,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_copies = (int)value;
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 4, G2V_EINVAL, "debug write mode out of [0, 4]");
+      REQUIRE(value >= 0 && value <= 5, G2V_EINVAL, "debug write mode out of [0, 5]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_GRID:
@@ -541,15 +542,23 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
   for (int32_t i = 0; i < c->V; ++i)
     REQUIRE(counts[i] > 0, G2V_EINVAL, "counts[%d] = %lld must be > 0", i, (long long)counts[i]);
   {
-    // staleness budget of the Hogwild grid (default_grid)
-    double zn = 0.0;
-    std::vector<double> pn((size_t)c->V);
+    // staleness budget of the Hogwild grid (default_grid): u(r) = K p_neg(r) +
+    // p_tok(r), p_tok from the downsampled counts (launch_vocab's keep rule)
+    double zn = 0.0, zt = 0.0, total = 0.0;
+    std::vector<double> pn((size_t)c->V), pt((size_t)c->V);
+    for (int32_t i = 0; i < c->V; ++i) total += (double)counts[i];
+    double thr = total;
+    if (sample > 0.0 && sample < 1.0) thr = sample * total;
+    else if (sample >= 1.0) thr = (double)(int64_t)(sample * (3.0 + sqrt(5.0)) / 2.0);
     for (int32_t i = 0; i < c->V; ++i) {
-      pn[i] = pow((double)counts[i], ns_exponent);
+      const double v = (double)counts[i];
+      pn[i] = pow(v, ns_exponent);
       zn += pn[i];
+      pt[i] = v * std::min(1.0, (sqrt(v / thr) + 1.0) * (thr / v));
+      zt += pt[i];
     }
     double um = 0.0;
-    for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn);
+    for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn + pt[i] / zt);
     c->u_max = um;
     if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
   }
@@ -855,7 +864,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     }
   }
   s.stripe = c->stripe;
-  if (c->debug_write >= 3) {
+  if (c->debug_write == 3 || c->debug_write == 4) {
     const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
     const int64_t words = rows * c->ld * (c->debug_write == 4 ? 2 : 1);
     if ((rc = dev_reserve(c->stream, &c->dbg16, &c->dbg16_cap, words))) return rc;

@@ -101,10 +101,11 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
 // 2 no table writes, 3 packed-f16 atomics into a scratch table (half the atomic
 // bytes, tables never written: a throughput probe), 4 the production f32
-// atomics into that scratch table (tables never written)
+// atomics into that scratch table (tables never written), 5 production atomics
+// on syn1neg only, syn0 never written (the ceiling of any syn0-side combining)
 template <int WR>
 __device__ __forceinline__ void upd(float* p, float v) {
-  if (WR == 0 || WR == 4) atomicAdd(p, v);
+  if (WR == 0 || WR == 4 || WR == 5) atomicAdd(p, v);
   else if (WR == 1) *p = v;
 }
 
@@ -263,7 +264,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         float* row = upd_row<WR>(a, 1, tg[d], (cbase + d) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, g[d] * s1[64 * i + lane]);
       }
-      if (any) {
+      if (any && WR != 5) {
         float* row = upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies) + lane;
         for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, lf * sw[64 * i + lane]);
       }
@@ -283,7 +284,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           }
           const bool from_work = (q == NT);
           if (from_work) {
-            coef = any ? lf : 0.f;
+            coef = (any && WR != 5) ? lf : 0.f;
             row_t = input;
           }
           if (lane / tail < tpack && q <= NT && coef != 0.f) {
@@ -320,6 +321,10 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 4) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 4>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 5) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 5>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
   if (nv == 1 && a.debug_write == 3) {

@@ -113,7 +113,8 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         2 uncached (re-allocates, zero-filled) [0]
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
  *                         atomics, 2 no table writes, 3 packed-f16 / 4 f32
- *                         atomics into a scratch table [0]
+ *                         atomics into a scratch table, 5 syn1neg atomics only
+ *                         (syn0 never written) [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off [8] (values stay exact:
  *                         readers sum the copies, each launch folds them back) */

@@ -479,13 +479,15 @@ def test_sampler_at_c2_full_size_bit_exact():
     assert np.isfinite(g0).all() and np.isfinite(g1).all() and np.abs(g1).max() > 0
 
 
-@pytest.mark.parametrize("V,zipf_s", [(300, 1.0), (2000, 1.0), (300, 0.0)])
-def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s):
+@pytest.mark.parametrize("V,zipf_s,sample", [(300, 1.0, 1e-3), (2000, 1.0, 1e-3), (300, 0.0, 1e-3),
+                                             (3000, 1.0, 0.0)])
+def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s, sample):
     """Small vocabularies, where every row is hot: the default grid is cut by
     the staleness budget (waves x hottest-row updates per example), and the
     Hogwild objective stays within 0.5 % of the sequential oracle after 3
-    gensim iterations (Zipf 1.0 and uniform genes)."""
-    D, K, sample = 200, 5, 1e-3
+    gensim iterations (Zipf 1.0 and uniform genes; V 3,000 without
+    downsampling diverged at 318 workgroups under a negatives-only budget)."""
+    D, K = 200, 5
     n = 300000
     tok, counts, syn0 = _zipf_setup(n, V, D, K, sample, seed=31) if zipf_s else (None,) * 3
     if not zipf_s:
@@ -503,6 +505,8 @@ def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s):
     grid = eng.get_option(N.OPT_GRID)
     if zipf_s and V <= 300:
         assert grid < 512, grid  # hotter than C4: fewer waves in flight
+    if zipf_s and not sample:
+        assert grid <= 210, grid  # the top gene's tokens count too
     eng.set_weights(syn0, np.zeros((V, D), np.float32))
     eng.set_corpus(tok, sent_len=2)
     a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
@@ -511,10 +515,10 @@ def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s):
         al = E.job_alphas(js, n)
         eng.train(js, al, E.job_seeds(rs_g, len(js) - 1), N.MODE_HOGWILD)
         CO.train(tok, off, js, al.astype(np.float32), E.job_seeds(rs_c, len(js) - 1),
-                 CO.sample_int(counts, sample), True, CO.make_cum_table(counts), a0, a1,
+                 CO.sample_int(counts, sample), sample != 0, CO.make_cum_table(counts), a0, a1,
                  np.ones(V, np.float32), K)
     g0, g1 = eng.get_weights()
     eng.close()
     l_gpu = _eval_loss(g0, g1, tok, counts, K)
     l_ref = _eval_loss(a0, a1, tok, counts, K)
-    assert abs(l_gpu - l_ref) / l_ref < 0.005, (V, zipf_s, grid, l_gpu, l_ref)
+    assert abs(l_gpu - l_ref) / l_ref < 0.005, (V, zipf_s, sample, grid, l_gpu, l_ref)
