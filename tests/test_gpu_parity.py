@@ -506,7 +506,7 @@ def test_train_hogwild_small_vocabulary_tracks_oracle(V, zipf_s, sample):
     if zipf_s and V <= 300:
         assert grid < 512, grid  # hotter than C4: fewer waves in flight
     if zipf_s and not sample:
-        assert grid <= 210, grid  # the top gene's tokens count too
+        assert grid < 250, grid  # the top gene's tokens count too (negatives alone: 313)
     eng.set_weights(syn0, np.zeros((V, D), np.float32))
     eng.set_corpus(tok, sent_len=2)
     a0, a1 = syn0.copy(), np.zeros((V, D), np.float32)
