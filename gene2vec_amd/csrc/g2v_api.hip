@@ -106,6 +106,7 @@ struct g2v_ctx {
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
   int stripe_rows = 8, stripe_copies = 8;
+  int atomic_overlap = 1;
   float* stripe = nullptr;
   int64_t stripe_cap = 0;
   uint32_t* dbg16 = nullptr;  // ablation 3: packed-f16 atomic scratch [2][V + stripes][ld/2]
@@ -163,6 +164,7 @@ struct g2v_ctx {
   // parallel modes; the float32 running sum of SEQUENTIAL lives in [1])
   float* log_table = nullptr;
   double* d_loss = nullptr;
+  unsigned int* d_queue = nullptr;  // k_sgns_atomic work queue (one counter)
 
   // replica merge: snapshot of both tables at the last merge, touched-row counts
   float *merge0 = nullptr, *merge1 = nullptr, *merge_cnt = nullptr;
@@ -179,20 +181,17 @@ struct g2v_ctx {
 };
 
 // Hogwild staleness bound.  Every wave in flight holds one example whose
-// updates the others do not see yet.  What blows up is a hot row taking many
-// stale updates at once after the reference's sawtooth sets alpha back to
-// 0.025 on an already trained model.  A row's share of the updates per
+// updates the others do not see yet.  A row's share of the updates per
 // example is u(r) = K * p_neg(r) (syn1neg, unigram^0.75 negatives) + p_tok(r)
 // (its share of kept tokens: syn0 input and syn1neg centre); u_max = max_r.
-// Measured on MI355X (waves x u_max in brackets):
-//   C2 (V 24,447 Zipf, K 5, sample 1e-3, u 0.122): 512 workgroups [249] track
-//     the oracle through the 10-iteration schedule; 768 [374] diverge;
-//   C4 (V 60,000, D 512, K 15, u 0.267): 512 [546] diverge in the second
-//     epoch of a 10 M-pair corpus, 256 [273] and 128 [137] match the oracle;
-//   V 3,000 Zipf, sample 0 (u 0.308): 512 [630] and 318 [391] diverge,
-//     204 [251] and 128 [157] match the sequential oracle.
-// So waves x u_max <= kStaleBudget, never more than 2 workgroups per CU.
-constexpr double kStaleBudget = 250.0;
+// Too many waves x u_max and the sawtooth alpha restart diverges (round 2,
+// C4 at 546, V 3,000 sample 0 at 315); well before
+// that the Hogwild objective drifts from the sequential one (V 3,000, 200 k
+// pairs, 3 iterations, 5 seeds: +0.4 % at 262-428, +0.05-0.1 % at 125-214).
+// The pipelined kernel (G2V_OPT_ATOMIC_OVERLAP) reaches the atomic roof with
+// 1 workgroup per CU at C2 and ~0.5 at C4, so the budget is set at the
+// quiet end: waves x u_max <= 125 (C2 256 workgroups, C4 117, V 3,000 149).
+constexpr double kStaleBudget = 125.0;
 
 static int default_grid(int cus, int K, int nv, double u_max) {
   int g = std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
@@ -369,7 +368,7 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
       (rc = dev_alloc(&c->bkt, (size_t)kBuckets + 1)) ||
       (rc = dev_alloc(&c->d_counts, (size_t)c->V)) || (rc = dev_alloc(&c->d_cpow, (size_t)c->V)) ||
       (rc = dev_alloc(&c->d_counters, 4)) || (rc = dev_alloc(&c->log_table, kExpTableSize)) ||
-      (rc = dev_alloc(&c->d_loss, 2)))
+      (rc = dev_alloc(&c->d_loss, 2)) || (rc = dev_alloc(&c->d_queue, 1)))
     return bail(rc);
   c->syn0 = c->own0;
   c->syn1 = c->own1;
@@ -431,6 +430,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->d_counters);
   dev_free(c->log_table);
   dev_free(c->d_loss);
+  dev_free(c->d_queue);
   dev_free(c->merge0);
   dev_free(c->merge1);
   dev_free(c->merge_cnt);
@@ -503,6 +503,10 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value >= 0 && value <= 5, G2V_EINVAL, "debug write mode out of [0, 5]");
       c->debug_write = (int)value;
       return G2V_OK;
+    case G2V_OPT_ATOMIC_OVERLAP:
+      REQUIRE(value == 0 || value == 1, G2V_EINVAL, "atomic overlap must be 0 or 1");
+      c->atomic_overlap = (int)value;
+      return G2V_OK;
     case G2V_OPT_GRID:
       REQUIRE(value >= 0, G2V_EINVAL, "grid must be >= 0");
       c->grid_user = value > 0;
@@ -523,6 +527,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_DEBUG_WRITE: *out = c->debug_write; return G2V_OK;
     case G2V_OPT_STRIPE_ROWS: *out = c->stripe_rows; return G2V_OK;
     case G2V_OPT_STRIPE_COPIES: *out = c->stripe_copies; return G2V_OK;
+    case G2V_OPT_ATOMIC_OVERLAP: *out = c->atomic_overlap; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -852,9 +857,16 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.loss_f64 = c->d_loss;
   s.loss_f32 = reinterpret_cast<float*>(c->d_loss + 1);
   const bool atomic_kernel = mode == kModeHogwild && s.hot_rows >= c->V;
-  const bool striped = atomic_kernel && c->stripe_copies > 1 && c->stripe_rows > 0;
-  s.stripe_rows = striped ? std::min(c->stripe_rows, c->V) : 0;
+  // rows past what a 1 GiB stripe buffer holds stay unstriped (kStripeMaxBytes)
+  const int64_t max_rows =
+      c->stripe_copies > 1 ? kStripeMaxBytes / (2 * 4 * (int64_t)(c->stripe_copies - 1) * c->ld)
+                           : 0;
+  const int srows = (int)std::min<int64_t>(std::min(c->stripe_rows, c->V), max_rows);
+  const bool striped = atomic_kernel && c->stripe_copies > 1 && srows > 0;
+  s.stripe_rows = striped ? srows : 0;
   s.stripe_copies = striped ? c->stripe_copies : 1;
+  s.overlap = c->atomic_overlap;
+  s.queue = c->d_queue;
   int rc;
   if (striped) {
     const int64_t need = 2 * (int64_t)(s.stripe_copies - 1) * s.stripe_rows * c->ld;
@@ -871,6 +883,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
   }
   s.dbg16 = c->dbg16;
+  if (atomic_kernel) HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(unsigned int), c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timing) {
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;

@@ -26,6 +26,9 @@ constexpr int kBucketShift = 15;
 constexpr int kBuckets = 1 << (31 - kBucketShift);
 
 constexpr int kSampleThreads = 1024;
+// k_sgns_atomic addresses the stripe buffer with 32-bit buffer offsets and
+// masks unused copies with an offset past it: the buffer stays below 1 GiB
+constexpr int64_t kStripeMaxBytes = 1ll << 30;
 constexpr int kSgnsThreads = 256;
 constexpr int kChunk = 32;  // consecutive examples a wave trains per grid-stride step
 
@@ -89,6 +92,8 @@ struct SgnsArgs {
   float* stripe;            // [2][stripe_copies-1][stripe_rows][ld]
   int stripe_rows;
   int stripe_copies;        // 1 = off
+  int overlap;              // G2V_OPT_ATOMIC_OVERLAP
+  unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;

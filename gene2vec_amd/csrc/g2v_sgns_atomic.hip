@@ -34,28 +34,46 @@ struct ExRegs {
 };
 
 // row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
-// main row plus its stripe copies when t is a striped hot row
+// the main row ...
 template <int NV>
-__device__ __forceinline__ void load_row(float4 (&o)[NV], const SgnsArgs& a,
-                                         __amdgpu_buffer_rsrc_t rmain, int t, int tbl, int rowb,
-                                         int lane, const bool (&on)[NV]) {
+__device__ __forceinline__ void load_main(float4 (&o)[NV], __amdgpu_buffer_rsrc_t rmain, int t,
+                                          int rowb, int lane, const bool (&on)[NV]) {
   const int off = t * rowb + lane * 16;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     o[v] = on[v] ? bload4<0>(rmain, off + 1024 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
-  if (t < a.stripe_rows) {
-    const float* sb = a.stripe + (int64_t)tbl * (a.stripe_copies - 1) * a.stripe_rows * a.ld;
-    for (int c = 1; c < a.stripe_copies; ++c) {
-      const float4* sr = reinterpret_cast<const float4*>(
-          sb + ((int64_t)(c - 1) * a.stripe_rows + t) * a.ld);
+}
+
+// ... plus its stripe copies when t is a striped hot row (t < stripe_rows).
+// The copies are loaded kStripeBatch at a time and summed in copy order, so a
+// striped row costs one memory latency per batch, not one per copy; copies
+// past stripe_copies read an out-of-range offset (zeros, no memory access).
+constexpr int kStripeBatch = 7;
+constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
+template <int NV>
+__device__ __forceinline__ void add_stripes(float4 (&o)[NV], const SgnsArgs& a,
+                                            __amdgpu_buffer_rsrc_t rs, int t, int tbl, int rowb,
+                                            int lane, const bool (&on)[NV]) {
+  const int C = a.stripe_copies;
+  for (int c0 = 1; c0 < C; c0 += kStripeBatch) {
+    float4 q[kStripeBatch][NV];
+#pragma unroll
+    for (int j = 0; j < kStripeBatch; ++j) {
+      const int c = c0 + j;
+      const int base = c < C ? ((tbl * (C - 1) + (c - 1)) * a.stripe_rows + t) * rowb : kStripeOob;
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        q[j][v] = on[v] ? bload4<0>(rs, base + lane * 16 + 1024 * v)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int j = 0; j < kStripeBatch; ++j) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
-        if (!on[v]) continue;
-        const float4 q = sr[lane + 64 * v];
-        o[v].x += q.x;
-        o[v].y += q.y;
-        o[v].z += q.z;
-        o[v].w += q.w;
+        o[v].x += q[j][v].x;
+        o[v].y += q[j][v].y;
+        o[v].z += q[j][v].z;
+        o[v].w += q[j][v].w;
       }
     }
   }
@@ -75,27 +93,34 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
   return a.stripe + (((int64_t)tbl * (a.stripe_copies - 1) + (c - 1)) * a.stripe_rows + t) * a.ld;
 }
 
+// record e of the chunk staged in LDS (k_sgns_atomic stages each chunk's
+// records once): tg / input / alpha as wave-uniform scalars; every main row is
+// requested before the first striped row's copies are waited on
 template <int K, int NV>
-__device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a, int64_t e,
-                                             __amdgpu_buffer_rsrc_t r0,
-                                             __amdgpu_buffer_rsrc_t r1, int rowb, int lane,
-                                             const bool (&on)[NV]) {
-  const int32_t* r = a.rec + e * a.rec_stride;
+__device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
+                                             const int32_t* r, __amdgpu_buffer_rsrc_t r0,
+                                             __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
+                                             int rowb, int lane, const bool (&on)[NV]) {
   x.tg[0] = __builtin_amdgcn_readfirstlane(r[0]);
   x.input = __builtin_amdgcn_readfirstlane(r[1]);
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
 #pragma unroll
   for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
-  load_row<NV>(x.l1, a, r0, x.input, 0, rowb, lane, on);
+  load_main<NV>(x.l1, r0, x.input, rowb, lane, on);
 #pragma unroll
   for (int d = 0; d <= K; ++d) {
     if (x.tg[d] >= 0) {
-      load_row<NV>(x.rw[d], a, r1, x.tg[d], 1, rowb, lane, on);
+      load_main<NV>(x.rw[d], r1, x.tg[d], rowb, lane, on);
     } else {
 #pragma unroll
       for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  if (x.input < a.stripe_rows) add_stripes<NV>(x.l1, a, rs, x.input, 0, rowb, lane, on);
+#pragma unroll
+  for (int d = 0; d <= K; ++d)
+    if (x.tg[d] >= 0 && x.tg[d] < a.stripe_rows)
+      add_stripes<NV>(x.rw[d], a, rs, x.tg[d], 1, rowb, lane, on);
 }
 
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
@@ -103,23 +128,62 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // bytes, tables never written: a throughput probe), 4 the production f32
 // atomics into that scratch table (tables never written), 5 production atomics
 // on syn1neg only, syn0 never written (the ceiling of any syn0-side combining)
-template <int WR>
-__device__ __forceinline__ void upd(float* p, float v) {
-  if (WR == 0 || WR == 4 || WR == 5) atomicAdd(p, v);
-  else if (WR == 1) *p = v;
+//
+// One row's delta coef * src[0, D) as a FIXED 4 * NV wave-instructions: the
+// buffer resource spans the row's D floats, so lanes past D (and every lane of
+// a skipped row: live = false gives an empty resource) are dropped by the
+// range check and send nothing to memory.  The fixed, branch-free count lets
+// the compiler wait for the next example's row loads with vmcnt(#atomics)
+// instead of draining this example's atomics (vmcnt(0)) -- atomics retire in
+// the background while the wave computes.
+template <int NV, int WR>
+__device__ __forceinline__ void emit_row(float* row, bool live, int D, const float* src, float coef,
+                                         int lane) {
+  // row and live are wave-uniform; say so, or the compiler waterfalls the resource
+  const uint64_t pa = reinterpret_cast<uint64_t>(row);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
+  const int nrec = __builtin_amdgcn_readfirstlane(live ? D * 4 : 0);
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), (short)0, nrec, 0x00020000);
+#pragma unroll
+  for (int i = 0; i < 4 * NV; ++i) {
+    const int off = (64 * i + lane) * 4;
+    const float v = coef * src[64 * i + lane];
+    if (WR == 0 || WR == 4 || WR == 5)
+      __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
+    else if (WR == 1)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
+  }
 }
 
 // LOSS ([ext] compute_loss): each wave keeps a float32 partial of the
 // -log(sigmoid(+-f)) LOG_TABLE terms over its chunk and adds it to a double
 // accumulator once per chunk; LOSS = false compiles the tally out.
+// Chunks of kChunk consecutive examples are handed out by a work queue (one
+// counter, lane 0's returning atomic): every wave works near the front of
+// the record stream whatever its speed.  With a static grid-stride split,
+// waves that share a CU (grid not a multiple of the CU count) fall behind
+// and apply early, high-alpha examples to a model the others have already
+// moved on: C2 vocabulary at 266 workgroups drifted +0.42 % from the
+// sequential objective, 256 and 300 stayed within 0.1 %.
+__device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
+  unsigned int v = 0;
+  if (lane == 0) v = atomicAdd(q, 1u);
+  return (int64_t)__builtin_amdgcn_readfirstlane(v);
+}
+
 template <int K, int NV, int WR = 0, bool LOSS = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
+  constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
   __shared__ float s_lut[kExpTableSize];
   __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
   __shared__ float s_wk[W][256 * NV];
+  __shared__ int32_t s_rec[W][kChunk * RS];  // the wave's chunk of records
+  __shared__ float s_lf[W][kChunk];          // lockf[input] per record of the chunk
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
     s_lut[i] = a.exp_table[i];
     if (LOSS) s_log[i] = a.log_table[i];
@@ -127,31 +191,47 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int64_t gw = (int64_t)blockIdx.x * W + wid;
-  const int64_t nw = (int64_t)gridDim.x * W;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t E = *a.n_examples;
   const int D = a.D;
-  const int full = D >> 6;           // whole 64-float atomic groups per row
-  const int tail = D & 63;           // leftover floats per row
-  const int tpack = tail ? 64 / tail : 0;  // row tails per packed instruction
   const int64_t tbytes = (int64_t)a.V * a.ld * 4;
   const __amdgpu_buffer_rsrc_t r0 = make_rsrc(a.rd0, tbytes);
   const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.rd1, tbytes);
+  const __amdgpu_buffer_rsrc_t rs =
+      make_rsrc(a.stripe, 2 * (int64_t)(a.stripe_copies - 1) * a.stripe_rows * a.ld * 4);
   const int rowb = (int)a.ld * 4;
   float* s1 = s_l1[wid];
   float* sw = s_wk[wid];
+  int32_t* sr = s_rec[wid];
+  float* slf = s_lf[wid];
   bool on[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) on[v] = (lane + 64 * v) < a.nvec;
 
-  for (int64_t c = gw; c * kChunk < E; c += nw) {
+  for (int64_t c = next_chunk(a.queue, lane); c * kChunk < E; c = next_chunk(a.queue, lane)) {
     const int64_t e_beg = c * kChunk;
     const int64_t e_end = (e_beg + kChunk < E) ? e_beg + kChunk : E;
+    // stage the chunk's records and their lockf once: per example, only row
+    // loads and atomics are vector-memory operations
+    {
+      const int nint = (int)(e_end - e_beg) * RS;
+      const int32_t* rb = a.rec + e_beg * RS;
+      for (int i = lane; i < nint; i += 64) sr[i] = rb[i];
+      __builtin_amdgcn_wave_barrier();
+      if (lane < e_end - e_beg) slf[lane] = a.lockf[sr[lane * RS + 1]];
+      __builtin_amdgcn_wave_barrier();
+    }
+    const int cb0 = (int)(e_beg % (int64_t)a.stripe_copies);
     float lsum = 0.f;
     ExRegs<K, NV> x;
-    load_example<K, NV>(x, a, e_beg, r0, r1, rowb, lane, on);
+    load_example<K, NV>(x, a, sr, r0, r1, rs, rowb, lane, on);
+    // drain here, so the loop head only waits on the back edge's count
+    // (vmcnt(#atomics of the previous example)); without it the two incoming
+    // paths merge to vmcnt(0), which also waits for the previous atomics
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
     for (int64_t e = e_beg; e < e_end; ++e) {
+      const int q = (int)(e - e_beg);
+      if (!a.overlap) __builtin_amdgcn_s_waitcnt(0x0F70);  // e-1's atomics land first
       // ---- compute example e ------------------------------------------------
       double pd[NT], dot[NT];
 #pragma unroll
@@ -166,11 +246,13 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int v = 0; v < NV; ++v) work[v] = make_float4(0.f, 0.f, 0.f, 0.f);
       float g[NT];
+      bool live[NT];  // wave-uniform: row d takes an update
       bool dirty[NT];
       bool any = false;
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         g[d] = 0.f;
+        live[d] = false;
         dirty[d] = false;
         if (x.tg[d] < 0) continue;
         double dt = dot[d];
@@ -210,6 +292,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           x.rw[d][v].w = __fmaf_rn(gg, x.l1[v].w, x.rw[d][v].w);
         }
         g[d] = gg;
+        live[d] = true;
         dirty[d] = true;
         any = true;
       }
@@ -224,13 +307,18 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int d = 0; d < NT; ++d) tg[d] = x.tg[d];
       const int32_t input = x.input;
-      const float lf = any ? a.lockf[input] : 0.f;
+      const float lf = slf[q];
 
       // ---- prefetch example e+1 (its loads overtake e's atomics) -------------
-      if (e + 1 < e_end) load_example<K, NV>(x, a, e + 1, r0, r1, rowb, lane, on);
+      // e-1's atomics retired behind e's compute; they must have landed before
+      // e+1 reads rows (a wave sees its own updates two examples back, as
+      // before this pipelining: the Hogwild staleness stays what the grid
+      // budget was measured with)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rowb, lane, on);
 
       // ---- atomics of example e -----------------------------------------------
-      const int cbase = (int)(e % (int64_t)a.stripe_copies);
+      const int cbase = (cb0 + q) % a.stripe_copies;
       if (WR == 3) {
         typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
         const int hw = (int)(a.ld >> 1);
@@ -258,42 +346,13 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         __builtin_amdgcn_wave_barrier();
         continue;
       }
+      // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work
 #pragma unroll
-      for (int d = 0; d < NT; ++d) {
-        if (g[d] == 0.f) continue;
-        float* row = upd_row<WR>(a, 1, tg[d], (cbase + d) % a.stripe_copies) + lane;
-        for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, g[d] * s1[64 * i + lane]);
-      }
-      if (any && WR != 5) {
-        float* row = upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies) + lane;
-        for (int i = 0; i < full; ++i) upd<WR>(row + 64 * i, lf * sw[64 * i + lane]);
-      }
-      if (tail && any) {
-        // rows q = 0..K: syn1neg[tg[q]] += g[q] * l1; q = K+1: syn0[input] += lf * work
-        for (int q0 = 0; q0 < NT + 1; q0 += tpack) {
-          const int q = q0 + lane / tail;
-          const int el = full * 64 + lane % tail;
-          float coef = 0.f;
-          int row_t = 0;
-#pragma unroll
-          for (int d = 0; d < NT; ++d) {
-            if (q == d) {
-              coef = g[d];
-              row_t = tg[d] < 0 ? 0 : tg[d];
-            }
-          }
-          const bool from_work = (q == NT);
-          if (from_work) {
-            coef = (any && WR != 5) ? lf : 0.f;
-            row_t = input;
-          }
-          if (lane / tail < tpack && q <= NT && coef != 0.f) {
-            const float src = from_work ? sw[el] : s1[el];
-            float* row = upd_row<WR>(a, from_work ? 0 : 1, row_t, (cbase + q) % a.stripe_copies);
-            upd<WR>(row + el, coef * src);
-          }
-        }
-      }
+      for (int d = 0; d < NT; ++d)
+        emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, (cbase + d) % a.stripe_copies),
+                         live[d], D, s1, g[d], lane);
+      emit_row<NV, WR>(upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies),
+                       any && WR != 5, D, sw, lf, lane);
       __builtin_amdgcn_wave_barrier();
     }
     if (LOSS && lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);

@@ -117,7 +117,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         (syn0 never written) [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off [8] (values stay exact:
- *                         readers sum the copies, each launch folds them back) */
+ *                         readers sum the copies, each launch folds them back)
+ *   G2V_OPT_ATOMIC_OVERLAP Hogwild kernel: 1 = a wave's table atomics retire
+ *                         behind its next example's compute, 0 = they land
+ *                         before it (less staleness per wave, more waves
+ *                         needed for the same rate) [1] */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
@@ -126,6 +130,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_DEBUG_WRITE 6
 #define G2V_OPT_STRIPE_ROWS 7
 #define G2V_OPT_STRIPE_COPIES 8
+#define G2V_OPT_ATOMIC_OVERLAP 9
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest

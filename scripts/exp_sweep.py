@@ -81,6 +81,8 @@ def main():
             eng.set_option(N.OPT_SEG_JOBS, int(cfg["seg"]))
         if "dbg" in cfg:
             eng.set_option(N.OPT_DEBUG_WRITE, int(cfg["dbg"]))
+        if "ov" in cfg:
+            eng.set_option(N.OPT_ATOMIC_OVERLAP, int(cfg["ov"]))
         mode = N.MODE_SEQUENTIAL if cfg.get("mode") == "seq" else N.MODE_HOGWILD
         stream = torch.cuda.Stream(dev)
         eng.set_stream(stream.cuda_stream)

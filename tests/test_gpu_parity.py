@@ -322,11 +322,15 @@ def _eval_loss(syn0, syn1, tok, counts, K, n_eval=20000, seed=99):
     return O.sgns_loss(syn0, syn1, c, j, negs)
 
 
-@pytest.mark.parametrize("D,K,seg_jobs", [(200, 5, 0), (512, 15, 0), (200, 5, 7)])
-def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs):
+@pytest.mark.parametrize("D,K,seg_jobs,overlap",
+                         [(200, 5, 0, 1), (512, 15, 0, 1), (200, 5, 7, 1), (200, 5, 0, 0)])
+def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs, overlap):
     """Hogwild GPU vs the sequential oracle on the same jobs/seeds: the SGNS
     objective on held-in pairs must agree within 0.5 % (Hogwild reorders
-    updates; it is judged end-to-end; measured 0.01-0.1 %)."""
+    updates; it is judged end-to-end).  Measured at the
+    default grid over 5 seed streams: -0.06..+0.11 %, mean +0.05 %; the
+    sequential oracle's own seed-to-seed spread is 0.5 %
+    (profiles/r02_hogwild_dev.log).  overlap = G2V_OPT_ATOMIC_OVERLAP."""
     sample = 1e-3
     tok, counts, syn0 = _zipf_setup(200000, 3000, D, K, sample)
     V = len(counts)
@@ -335,6 +339,7 @@ def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs):
     eng = E.SGNSEngine(V, D, K)
     if seg_jobs:
         eng.set_option(N.OPT_SEG_JOBS, seg_jobs)  # pipelined sampler/SGNS segments
+    eng.set_option(N.OPT_ATOMIC_OVERLAP, overlap)
     eng.set_vocab(counts, sample)
     eng.set_weights(syn0, np.zeros((V, D), np.float32))
     eng.set_corpus(tok, sent_len=2)
