@@ -93,7 +93,7 @@ def parse():
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                         "the N>1 path with several ranks sharing one GPU)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02c.json"))
     return p.parse_args()
 
 
