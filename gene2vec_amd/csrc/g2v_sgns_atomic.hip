@@ -137,8 +137,8 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // instead of draining this example's atomics (vmcnt(0)) -- atomics retire in
 // the background while the wave computes.
 template <int NV, int WR>
-__device__ __forceinline__ void emit_row(float* row, bool live, int D, const float* src, float coef,
-                                         int lane) {
+__device__ __forceinline__ void emit_row(float* row, bool live, int D, const float (&src)[4 * NV],
+                                         float coef, int lane) {
   // row and live are wave-uniform; say so, or the compiler waterfalls the resource
   const uint64_t pa = reinterpret_cast<uint64_t>(row);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa);
@@ -149,7 +149,7 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 #pragma unroll
   for (int i = 0; i < 4 * NV; ++i) {
     const int off = (64 * i + lane) * 4;
-    const float v = coef * src[64 * i + lane];
+    const float v = coef * src[i];
     if (WR == 0 || WR == 4 || WR == 5)
       __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
     else if (WR == 1)
@@ -245,6 +245,20 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       float4 work[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) work[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      // sigmoid (and LOG_TABLE) lookups of all K+1 dots issued together, not
+      // one dependent LDS round trip per row; a duplicate of an updated row
+      // recomputes its dot and looks up again below
+      float fv[NT], lv[NT], lg[NT];
+#pragma unroll
+      for (int d = 0; d < NT; ++d) {
+        fv[d] = (float)dot[d];
+        const bool in = fv[d] > -(float)kMaxExp && fv[d] < (float)kMaxExp;
+        lv[d] = s_lut[in ? (int)((fv[d] + (float)kMaxExp) * (float)kLutScale) : 0];
+        if (LOSS) {
+          const float fl = d == 0 ? fv[d] : -fv[d];
+          lg[d] = s_log[in ? (int)((fl + (float)kMaxExp) * (float)kLutScale) : 0];
+        }
+      }
       float g[NT];
       bool live[NT];  // wave-uniform: row d takes an update
       bool dirty[NT];
@@ -255,7 +269,6 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         live[d] = false;
         dirty[d] = false;
         if (x.tg[d] < 0) continue;
-        double dt = dot[d];
         bool prev_dirty = false;
 #pragma unroll
         for (int d2 = 0; d2 < d; ++d2) {
@@ -265,21 +278,24 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
             prev_dirty = dirty[d2];
           }
         }
+        float f = fv[d], lut = lv[d], lgv = LOSS ? lg[d] : 0.f;
         if (prev_dirty) {
           double s = 0.0;
 #pragma unroll
           for (int v = 0; v < NV; ++v) s = dot4(x.l1[v], x.rw[d][v], s);
-          dt = wave_allreduce_d(s);
+          f = (float)wave_allreduce_d(s);
           dirty[d] = true;
+          if (f > -(float)kMaxExp && f < (float)kMaxExp) {
+            lut = s_lut[(int)((f + (float)kMaxExp) * (float)kLutScale)];
+            if (LOSS) {
+              const float fl = d == 0 ? f : -f;
+              lgv = s_log[(int)((fl + (float)kMaxExp) * (float)kLutScale)];
+            }
+          }
         }
-        const float f = (float)dt;
         if (f <= -(float)kMaxExp || f >= (float)kMaxExp) continue;
-        const int idx = (int)((f + (float)kMaxExp) * (float)kLutScale);
-        const float gg = ((d == 0 ? 1.0f : 0.0f) - s_lut[idx]) * x.alpha;
-        if (LOSS) {
-          const float fl = d == 0 ? f : -f;
-          lsum = lsum - s_log[(int)((fl + (float)kMaxExp) * (float)kLutScale)];
-        }
+        const float gg = ((d == 0 ? 1.0f : 0.0f) - lut) * x.alpha;
+        if (LOSS) lsum = lsum - lgv;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
           work[v].x = __fmaf_rn(gg, x.rw[d][v].x, work[v].x);
@@ -303,6 +319,13 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         *reinterpret_cast<float4*>(sw + (lane + 64 * v) * 4) = work[v];
       }
       __builtin_amdgcn_wave_barrier();
+      // this lane's elements 64 i + lane of l1 and work, read back once for all rows
+      float v1[4 * NV], vw[4 * NV];
+#pragma unroll
+      for (int i = 0; i < 4 * NV; ++i) {
+        v1[i] = s1[64 * i + lane];
+        vw[i] = sw[64 * i + lane];
+      }
       int32_t tg[NT];
 #pragma unroll
       for (int d = 0; d < NT; ++d) tg[d] = x.tg[d];
@@ -350,9 +373,9 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int d = 0; d < NT; ++d)
         emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, (cbase + d) % a.stripe_copies),
-                         live[d], D, s1, g[d], lane);
+                         live[d], D, v1, g[d], lane);
       emit_row<NV, WR>(upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies),
-                       any && WR != 5, D, sw, lf, lane);
+                       any && WR != 5, D, vw, lf, lane);
       __builtin_amdgcn_wave_barrier();
     }
     if (LOSS && lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);
