@@ -349,7 +349,9 @@ def main():
                              f"{world}, dim {D}, neg {K}, replica merge ({a.merge}) every "
                              f"{avg_every} jobs: "
                              + ("libg2v g2v_average (RCCL over xGMI)" if merge_backend == "rccl"
-                                else "torch.distributed gloo rehearsal, ranks sharing a GPU")),
+                                else "torch.distributed gloo rehearsal, ranks sharing a GPU"
+                                if a.backend == "gloo" else
+                                "torch.distributed merge (libg2v communicator unavailable)")),
                 "vocab": V, "pairs_per_gpu": n_pairs, "dim": D, "negative": K,
                 "sample": a.sample, "window": 1,
                 "parallelism": f"dp{world}" + (f" + {merge_backend} {a.merge} merge"

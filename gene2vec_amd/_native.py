@@ -112,6 +112,7 @@ SIGNATURES = {
     "g2v_corpus_info": (C.c_int, [_vp, C.POINTER(_i64), C.POINTER(_i64), C.POINTER(_i64),
                                   C.POINTER(_i64)]),
     "g2v_corpus_export": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
+    "g2v_corpus_sent_len": (C.c_int, [_vp, C.POINTER(_i64)]),
     "g2v_corpus_free": (C.c_int, [_vp]),
     "g2v_csr_permute": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "g2v_pairs_permute": (C.c_int, [_vp, _i64, _vp, _vp]),

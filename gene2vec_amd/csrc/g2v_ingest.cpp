@@ -19,6 +19,7 @@
 #include <stdio.h>
 #include <fcntl.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -75,11 +76,23 @@ struct Chunk {  // a line-aligned piece of one file
   const char* p = nullptr;
   size_t n = 0;
   std::vector<int32_t> tok;              // local ids
-  std::vector<int64_t> len;              // sentence lengths
+  int64_t lines = 0;                     // sentences in the chunk
+  int64_t fixed = -1;                    // their common length while len is empty (-1: none yet)
+  std::vector<int64_t> len;              // sentence lengths, once two lengths differ
   std::vector<std::string_view> words;   // local id -> bytes (views into the file buffer)
   std::vector<uint64_t> hash;            // local id -> hash_bytes(word)
   std::vector<int64_t> cnt;              // local counts
   int err = 0;
+  void end_line(int64_t ntok) {
+    if (len.empty() && (fixed < 0 || fixed == ntok)) {
+      fixed = ntok;  // pair files: every line 2 tokens, nothing stored
+    } else {
+      if (len.empty()) len.assign((size_t)lines, fixed);
+      len.push_back(ntok);
+    }
+    ++lines;
+  }
+  int64_t length(int64_t i) const { return len.empty() ? fixed : len[(size_t)i]; }
 };
 
 // open-addressing word -> id table (linear probing, load <= 1/2).  A slot
@@ -135,7 +148,6 @@ void tokenize(Chunk& c) {
   const unsigned char* s = (const unsigned char*)c.p;
   const size_t n = c.n;
   c.tok.reserve(n / 6 + 16);
-  c.len.reserve(n / 12 + 16);
   size_t i = 0;
   while (i < n) {
     // one line: up to '\n', '\r\n' or '\r'
@@ -163,7 +175,7 @@ void tokenize(Chunk& c) {
       c.tok.push_back((int32_t)id);
       ++ntok;
     }
-    c.len.push_back(ntok);
+    c.end_line(ntok);
     if (i < n) {  // consume the line terminator
       if (s[i] == '\r' && i + 1 < n && s[i + 1] == '\n') i += 2;
       else ++i;
@@ -187,10 +199,12 @@ void parallel_for(size_t n, int threads, Fn&& fn) {
 }  // namespace
 
 struct g2v_corpus {
-  std::vector<std::string> files;     // file contents (owned buffers)
-  std::vector<int32_t> tok;
-  std::vector<int64_t> off;
-  std::vector<std::string> words;     // global id -> bytes (windows-1252)
+  std::vector<Chunk> chunks;                   // tokens in chunk-local ids
+  std::vector<std::vector<int32_t>> remap;     // chunk-local id -> global id
+  std::vector<int64_t> tbase, sbase;           // token / sentence offset of each chunk
+  int64_t fixed_len = -1;                      // common sentence length, -1 = ragged
+  int threads = 8;
+  std::vector<std::string> words;              // global id -> bytes (windows-1252)
   std::vector<int64_t> counts;
 };
 
@@ -202,57 +216,51 @@ int g2v_corpus_read(const char* const* paths, int n_paths, int n_threads, g2v_co
   std::unique_ptr<g2v_corpus> cp(new (std::nothrow) g2v_corpus());
   if (!cp) return G2V_ENOMEM;
   const int threads = n_threads > 0 ? n_threads : 8;
-  // whole files into owned buffers, 64 MiB pieces read in parallel (pread)
-  constexpr size_t kPiece = (size_t)64 << 20;
-  cp->files.resize(n_paths);
-  std::vector<int> fds(n_paths, -1);
-  struct Piece {
-    int f;
-    size_t off, n;
-  };
-  std::vector<Piece> pieces;
-  bool bad = false;
-  for (int f = 0; f < n_paths; ++f) {
-    fds[f] = open(paths[f], O_RDONLY);
-    struct stat st;
-    if (fds[f] < 0 || fstat(fds[f], &st) != 0) {
-      bad = true;
-      break;
+  cp->threads = threads;
+  // files mapped read-only from the page cache (no copy, no zero-filled
+  // buffer); unmapped when the read returns (words are copied out, tokens are
+  // ids)
+  struct Map {
+    const char* p = nullptr;
+    size_t n = 0;
+    ~Map() {
+      if (p && n) munmap(const_cast<char*>(p), n);
     }
-    cp->files[f].resize((size_t)st.st_size);
-    for (size_t o = 0; o < (size_t)st.st_size; o += kPiece)
-      pieces.push_back({f, o, std::min(kPiece, (size_t)st.st_size - o)});
-  }
-  std::atomic<bool> io_err{false};
-  if (!bad)
-    parallel_for(pieces.size(), threads, [&](size_t k) {
-      const Piece& p = pieces[k];
-      size_t got = 0;
-      while (got < p.n) {
-        const ssize_t r = pread(fds[p.f], &cp->files[p.f][p.off + got], p.n - got,
-                                (off_t)(p.off + got));
-        if (r <= 0) {
-          io_err = true;
-          return;
-        }
-        got += (size_t)r;
+  };
+  std::vector<Map> maps(n_paths);
+  for (int f = 0; f < n_paths; ++f) {
+    const int fd = open(paths[f], O_RDONLY);
+    struct stat st;
+    if (fd < 0 || fstat(fd, &st) != 0) {
+      if (fd >= 0) close(fd);
+      return G2V_EINVAL;
+    }
+    maps[f].n = (size_t)st.st_size;
+    if (maps[f].n) {
+      void* m = mmap(nullptr, maps[f].n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+      if (m == MAP_FAILED) {
+        maps[f].n = 0;
+        close(fd);
+        return G2V_EINVAL;
       }
-    });
-  for (int fd : fds)
-    if (fd >= 0) close(fd);
-  if (bad || io_err) return G2V_EINVAL;
+      maps[f].p = static_cast<const char*>(m);
+    }
+    close(fd);
+  }
   // line-aligned chunks of ~16 MiB, in file order
-  std::vector<Chunk> chunks;
+  std::vector<Chunk>& chunks = cp->chunks;
   const size_t target = (size_t)16 << 20;
-  for (auto& buf : cp->files) {
+  for (int f = 0; f < n_paths; ++f) {
+    const char* buf = maps[f].p;
+    const size_t n = maps[f].n;
     size_t b = 0;
-    while (b < buf.size()) {
-      size_t e = std::min(buf.size(), b + target);
-      while (e < buf.size() && buf[e - 1] != '\n' && buf[e - 1] != '\r') ++e;
+    while (b < n) {
+      size_t e = std::min(n, b + target);
+      while (e < n && buf[e - 1] != '\n' && buf[e - 1] != '\r') ++e;
       // never split a "\r\n" pair
-      if (e < buf.size() && buf[e - 1] == '\r' && buf[e] == '\n') ++e;
+      if (e < n && buf[e - 1] == '\r' && buf[e] == '\n') ++e;
       Chunk c;
-      c.p = buf.data() + b;
+      c.p = buf + b;
       c.n = e - b;
       chunks.push_back(std::move(c));
       b = e;
@@ -262,14 +270,18 @@ int g2v_corpus_read(const char* const* paths, int n_paths, int n_threads, g2v_co
   for (auto& c : chunks)
     if (c.err) return G2V_EINVAL;  // UnicodeDecodeError in the reference
   // global ids in first-occurrence order = chunk order, then local order
-  // (sequential over each chunk's vocabulary only); token remap in parallel
+  // (sequential over each chunk's vocabulary only); the token remap itself
+  // runs in g2v_corpus_export, straight into the caller's buffer
   WordTable gtab(1 << 16);
   std::vector<std::string_view> gwords;
-  std::vector<std::vector<int32_t>> remap(chunks.size());
-  std::vector<size_t> tbase(chunks.size() + 1, 0), sbase(chunks.size() + 1, 0);
+  cp->remap.resize(chunks.size());
+  cp->tbase.assign(chunks.size() + 1, 0);
+  cp->sbase.assign(chunks.size() + 1, 0);
+  int64_t fixed = -2;  // -2: no sentence yet
   for (size_t k = 0; k < chunks.size(); ++k) {
     Chunk& c = chunks[k];
-    remap[k].resize(c.words.size());
+    std::vector<int32_t>& rm = cp->remap[k];
+    rm.resize(c.words.size());
     for (size_t l = 0; l < c.words.size(); ++l) {
       int64_t g = gtab.find(gwords, c.words[l], c.hash[l]);
       if (g < 0) {
@@ -278,26 +290,24 @@ int g2v_corpus_read(const char* const* paths, int n_paths, int n_threads, g2v_co
         gwords.push_back(c.words[l]);
         cp->counts.push_back(0);
       }
-      remap[k][l] = (int32_t)g;
+      rm[l] = (int32_t)g;
       cp->counts[(size_t)g] += c.cnt[l];
     }
-    tbase[k + 1] = tbase[k] + c.tok.size();
-    sbase[k + 1] = sbase[k] + c.len.size();
+    // views into the mapped files are not kept past the read
+    c.p = nullptr;
+    std::vector<uint64_t>().swap(c.hash);
+    std::vector<int64_t>().swap(c.cnt);
+    cp->tbase[k + 1] = cp->tbase[k] + (int64_t)c.tok.size();
+    cp->sbase[k + 1] = cp->sbase[k] + c.lines;
+    if (c.lines) {
+      const int64_t cf = c.len.empty() ? c.fixed : -1;
+      fixed = (fixed == -2 || fixed == cf) ? cf : -1;
+    }
   }
-  cp->tok.resize(tbase.back());
-  cp->off.resize(sbase.back() + 1);
-  cp->off[0] = 0;
-  parallel_for(chunks.size(), threads, [&](size_t k) {
-    const Chunk& c = chunks[k];
-    const int32_t* rm = remap[k].data();
-    int32_t* dst = cp->tok.data() + tbase[k];
-    for (size_t i = 0; i < c.tok.size(); ++i) dst[i] = rm[c.tok[i]];
-    int64_t o = (int64_t)tbase[k];
-    int64_t* od = cp->off.data() + sbase[k] + 1;
-    for (size_t i = 0; i < c.len.size(); ++i) od[i] = (o += c.len[i]);
-  });
+  cp->fixed_len = fixed == -2 ? -1 : fixed;
   cp->words.reserve(gwords.size());
   for (auto& w : gwords) cp->words.emplace_back(w);
+  for (auto& c : chunks) std::vector<std::string_view>().swap(c.words);
   *out = cp.release();
   return G2V_OK;
 }
@@ -305,8 +315,8 @@ int g2v_corpus_read(const char* const* paths, int n_paths, int n_threads, g2v_co
 int g2v_corpus_info(const g2v_corpus* c, int64_t* n_tokens, int64_t* n_sent, int64_t* n_words,
                     int64_t* word_bytes) {
   if (!c) return G2V_EINVAL;
-  if (n_tokens) *n_tokens = (int64_t)c->tok.size();
-  if (n_sent) *n_sent = (int64_t)c->off.size() - 1;
+  if (n_tokens) *n_tokens = c->tbase.empty() ? 0 : c->tbase.back();
+  if (n_sent) *n_sent = c->sbase.empty() ? 0 : c->sbase.back();
   if (n_words) *n_words = (int64_t)c->words.size();
   if (word_bytes) {
     int64_t b = 0;
@@ -316,13 +326,32 @@ int g2v_corpus_info(const g2v_corpus* c, int64_t* n_tokens, int64_t* n_sent, int
   return G2V_OK;
 }
 
+int g2v_corpus_sent_len(const g2v_corpus* c, int64_t* len) {
+  if (!c || !len) return G2V_EINVAL;
+  *len = c->fixed_len;
+  return G2V_OK;
+}
+
 // tokens[n_tokens], sent_off[n_sent+1], counts[n_words], words as concatenated
 // bytes + word_off[n_words+1]; any pointer may be NULL
 int g2v_corpus_export(const g2v_corpus* c, int32_t* tokens, int64_t* sent_off, int64_t* counts,
                       char* words, int64_t* word_off) {
   if (!c) return G2V_EINVAL;
-  if (tokens) memcpy(tokens, c->tok.data(), c->tok.size() * sizeof(int32_t));
-  if (sent_off) memcpy(sent_off, c->off.data(), c->off.size() * sizeof(int64_t));
+  if (sent_off) sent_off[0] = 0;
+  if (tokens || sent_off)
+    parallel_for(c->chunks.size(), c->threads, [&](size_t k) {
+      const Chunk& ch = c->chunks[k];
+      if (tokens) {
+        const int32_t* rm = c->remap[k].data();
+        int32_t* dst = tokens + c->tbase[k];
+        for (size_t i = 0; i < ch.tok.size(); ++i) dst[i] = rm[ch.tok[i]];
+      }
+      if (sent_off) {
+        int64_t o = c->tbase[k];
+        int64_t* od = sent_off + c->sbase[k] + 1;
+        for (int64_t i = 0; i < ch.lines; ++i) od[i] = (o += ch.length(i));
+      }
+    });
   if (counts) memcpy(counts, c->counts.data(), c->counts.size() * sizeof(int64_t));
   if (words || word_off) {
     int64_t b = 0;

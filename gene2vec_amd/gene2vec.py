@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import argparse
 import contextlib
+import copy
 import datetime
 import json
 import logging
@@ -171,6 +172,10 @@ def main(argv=None):
     parser.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                         help="data-parallel process group under torchrun (nccl = RCCL over "
                              "xGMI; gloo only to rehearse with ranks sharing a GPU)")
+    parser.add_argument("--reload-checkpoints", action="store_true",
+                        help="load every iteration's model back from the checkpoint just "
+                             "written, as src/gene2vec.py:86 does (the kept in-memory model "
+                             "is the same state: tables, vocabulary and RNG round-trip exactly)")
     parser.add_argument("--merge-every-jobs", type=int, default=1024,
                         help="data-parallel replica merge cadence (gensim jobs per rank)")
     args = parser.parse_args(argv)
@@ -230,6 +235,7 @@ def main(argv=None):
                   device=args.device, mode=args.mode, data_parallel=world > 1)
         import gene2vec_amd.word2vec as W
         W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
+        model = None
         for current_iter in range(1, args.iters + 1):
             name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")
             if current_iter == 1:
@@ -242,7 +248,7 @@ def main(argv=None):
                         model = Word2Vec(**kw)
                         model._build_from_counts(corpus.vocab_raw_counts())
                         model.corpus_count = corpus.n_sent
-                        model.corpus_total_words = int(corpus.sent_off[-1])
+                        model.corpus_total_words = int(len(corpus.tokens))
                         ids = _vocab_ids(model, corpus)
                         tok = ids[corpus.tokens]
                         _adopt_vocab_ids(corpus, ids, tok)
@@ -264,8 +270,13 @@ def main(argv=None):
                 print(f"gene2vec dimension {dimension} iteration {current_iter} start")
                 prev = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter - 1}")
                 with ph("load"):
-                    model = Word2Vec.load(prev, device=args.device)
-                    model.data_parallel = world > 1
+                    # src/gene2vec.py:86 reloads the checkpoint it just saved; the
+                    # model kept from the last iteration is that state (save/load
+                    # round-trips bit for bit), and its device tables and engine stay
+                    # resident.  Data-parallel ranks take rank 0's checkpoint.
+                    if args.reload_checkpoints or world > 1 or model is None:
+                        model = Word2Vec.load(prev, device=args.device)
+                        model.data_parallel = world > 1
                 if corpus is None:
                     with ph("train"):
                         model.train(gene_pairs, total_examples=model.corpus_count,
@@ -288,13 +299,15 @@ def main(argv=None):
                 # the text exports (generateMatrix.py, save_word2vec_format) read
                 # this iteration's checkpoint / tables only: they run on a host
                 # thread while the next iteration trains (one at a time, in order)
-                exporter.submit(name, model.wv, ph)
+                # a snapshot: the next iteration rebinds model.wv's arrays
+                exporter.submit(name, copy.copy(model.wv), ph)
             if world > 1:
                 import torch.distributed as dist
                 dist.barrier()  # the next iteration loads rank 0's checkpoint
             print(f"gene2vec dimension {dimension} iteration {current_iter} done")
             outputs.append(name)
-            del model
+            if args.reload_checkpoints or world > 1:
+                model = None  # freed (device tables too) before the reload
     finally:
         if pipe is not None:
             pipe.close(wait=True)

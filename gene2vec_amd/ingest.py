@@ -20,23 +20,42 @@ from . import engine as E
 
 
 class Corpus:
-    def __init__(self, tokens, sent_off, words, counts):
+    def __init__(self, tokens, sent_off, words, counts, sent_len=0):
         self.tokens = tokens        # int32[n_tokens], ids into words
-        self.sent_off = sent_off    # int64[n_sent + 1]
+        # int64[n_sent + 1]; None when every sentence has sent_len tokens (pair
+        # files: the 8-byte offset per pair is never materialised)
+        self._sent_off = sent_off
+        self._sent_len = int(sent_len)
         self.words = words          # list[str], first-occurrence order
         self.counts = counts        # int64[n_words]
 
     @property
+    def sent_off(self):
+        if self._sent_off is None:
+            n = len(self.tokens) // self._sent_len
+            self._sent_off = np.arange(0, self._sent_len * n + 1, self._sent_len, dtype=np.int64)
+        return self._sent_off
+
+    @sent_off.setter
+    def sent_off(self, v):
+        self._sent_off = v
+
+    @property
     def n_sent(self):
-        return len(self.sent_off) - 1
+        if self._sent_off is None:
+            return len(self.tokens) // self._sent_len
+        return len(self._sent_off) - 1
 
     @property
     def pairs_only(self):
         """every sentence is exactly 2 tokens (the pair generator's output);
         checked once, permutations keep it"""
         if getattr(self, "_pairs_only", None) is None:
-            self._pairs_only = bool(np.array_equal(
-                self.sent_off, np.arange(0, 2 * self.n_sent + 1, 2, dtype=np.int64)))
+            if self._sent_off is None:
+                self._pairs_only = self._sent_len == 2
+            else:
+                self._pairs_only = bool(np.array_equal(
+                    self._sent_off, np.arange(0, 2 * self.n_sent + 1, 2, dtype=np.int64)))
         return self._pairs_only
 
     def sentences(self):
@@ -101,18 +120,21 @@ def read_corpus(paths, threads=None):
     try:
         nt, ns, nw, nb = C.c_int64(), C.c_int64(), C.c_int64(), C.c_int64()
         N.check(L.g2v_corpus_info(h, C.byref(nt), C.byref(ns), C.byref(nw), C.byref(nb)))
+        sl = C.c_int64()
+        N.check(L.g2v_corpus_sent_len(h, C.byref(sl)))
         tok = np.empty(nt.value, np.int32)
-        off = np.empty(ns.value + 1, np.int64)
+        # fixed-length sentences (pair files): offsets stay implicit
+        off = None if sl.value == 2 else np.empty(ns.value + 1, np.int64)
         counts = np.empty(nw.value, np.int64)
         wbytes = np.empty(max(nb.value, 1), np.uint8)
         woff = np.empty(nw.value + 1, np.int64)
-        N.check(L.g2v_corpus_export(h, N.ptr(tok), N.ptr(off), N.ptr(counts), N.ptr(wbytes),
-                                    N.ptr(woff)))
+        N.check(L.g2v_corpus_export(h, N.ptr(tok), N.ptr(off) if off is not None else None,
+                                    N.ptr(counts), N.ptr(wbytes), N.ptr(woff)))
     finally:
         L.g2v_corpus_free(h)
     raw = wbytes.tobytes()
     words = [raw[woff[i]:woff[i + 1]].decode("windows-1252") for i in range(nw.value)]
-    return Corpus(tok, off, words, counts)
+    return Corpus(tok, off, words, counts, sent_len=2 if off is None else 0)
 
 
 def py_shuffle_perm(n, rng: random.Random, out=None):

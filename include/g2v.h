@@ -321,6 +321,9 @@ int g2v_corpus_info(const g2v_corpus *c, int64_t *n_tokens, int64_t *n_sent, int
                     int64_t *word_bytes);
 int g2v_corpus_export(const g2v_corpus *c, int32_t *tokens, int64_t *sent_off, int64_t *counts,
                       char *words, int64_t *word_off);
+/* The length every sentence of the corpus has (2 for the pair generator's
+ * files: sent_off is then implicit and need not be exported), -1 if ragged. */
+int g2v_corpus_sent_len(const g2v_corpus *c, int64_t *len);
 int g2v_corpus_free(g2v_corpus *c);
 /* out sentence i = in sentence perm[i] (CSR gather) */
 int g2v_csr_permute(const int32_t *tok, const int64_t *off, int64_t n_sent, const int64_t *perm,

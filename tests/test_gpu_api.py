@@ -82,6 +82,28 @@ def test_cli_end_to_end_matches_oracle(tmp_path, test_pairs):
                                rtol=1e-5, atol=1e-7)
 
 
+def test_cli_kept_model_equals_reloaded_checkpoints(tmp_path):
+    """The CLI keeps iteration n's model for iteration n+1 instead of loading
+    the checkpoint it has just written (src/gene2vec.py:86): the exports of
+    both ways are byte-identical (sequential mode, so the run is
+    deterministic)."""
+    data = tmp_path / "data"
+    data.mkdir()
+    rng = np.random.RandomState(5)
+    genes = [f"G{i}" for i in range(300)]
+    lines = [f"{genes[a]} {genes[b]}" for a, b in rng.randint(0, 300, (4000, 2)) if a != b]
+    (data / "s.txt").write_text("\n".join(lines) + "\n")
+    got = {}
+    for tag, extra in (("kept", []), ("reload", ["--reload-checkpoints"])):
+        out = tmp_path / tag
+        cli_main([str(data), str(out), "txt", "--iters", "3", "--dim", "64", "--mode",
+                  "sequential", "--hash", "crc32", "--shuffle-seed", "5", "--native-ingest"]
+                 + extra)
+        got[tag] = [open(out / f"gene2vec_dim_64_iter_{n}{suf}", "rb").read()
+                    for n in (1, 2, 3) for suf in (".txt", "_w2v.txt")]
+    assert got["kept"] == got["reload"]
+
+
 @pytest.mark.parametrize("ragged", [False, True])
 def test_cli_native_ingest_equals_python_ingest(tmp_path, ragged):
     """all-pairs files take the pair-gather / fixed-length path, ragged ones
