@@ -113,6 +113,7 @@ SIGNATURES = {
                                   C.POINTER(_i64)]),
     "g2v_corpus_export": (C.c_int, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "g2v_corpus_sent_len": (C.c_int, [_vp, C.POINTER(_i64)]),
+    "g2v_count_lines": (C.c_int, [_vp, C.c_int, C.c_int, C.POINTER(_i64)]),
     "g2v_corpus_free": (C.c_int, [_vp]),
     "g2v_csr_permute": (C.c_int, [_vp, _vp, _i64, _vp, _vp, _vp]),
     "g2v_pairs_permute": (C.c_int, [_vp, _i64, _vp, _vp]),

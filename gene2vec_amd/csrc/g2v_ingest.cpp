@@ -326,6 +326,45 @@ int g2v_corpus_info(const g2v_corpus* c, int64_t* n_tokens, int64_t* n_sent, int
   return G2V_OK;
 }
 
+int g2v_count_lines(const char* const* paths, int n_paths, int n_threads, int64_t* out) {
+  if (!out || (n_paths > 0 && !paths) || n_paths < 0) return G2V_EINVAL;
+  *out = 0;
+  const int threads = n_threads > 0 ? n_threads : 8;
+  std::atomic<int64_t> total{0};
+  for (int f = 0; f < n_paths; ++f) {
+    const int fd = open(paths[f], O_RDONLY);
+    struct stat st;
+    if (fd < 0 || fstat(fd, &st) != 0) {
+      if (fd >= 0) close(fd);
+      return G2V_EINVAL;
+    }
+    const size_t n = (size_t)st.st_size;
+    if (n == 0) {
+      close(fd);
+      continue;
+    }
+    void* m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE | MAP_POPULATE, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) return G2V_EINVAL;
+    const unsigned char* b = static_cast<const unsigned char*>(m);
+    // universal newlines, as the tokenizer splits: '\n', "\r\n" and a lone
+    // '\r' end a line; an unterminated last line is a line too
+    constexpr size_t kPiece = (size_t)16 << 20;
+    const size_t pieces = (n + kPiece - 1) / kPiece;
+    parallel_for(pieces, threads, [&](size_t k) {
+      const size_t lo = k * kPiece, hi = std::min(n, lo + kPiece);
+      int64_t c = 0;
+      for (size_t i = lo; i < hi; ++i)
+        c += (b[i] == '\n') + (b[i] == '\r' && (i + 1 == n || b[i + 1] != '\n'));
+      total += c;
+    });
+    if (b[n - 1] != '\n' && b[n - 1] != '\r') total += 1;
+    munmap(m, n);
+  }
+  *out = total.load();
+  return G2V_OK;
+}
+
 int g2v_corpus_sent_len(const g2v_corpus* c, int64_t* len) {
   if (!c || !len) return G2V_EINVAL;
   *len = c->fixed_len;

@@ -193,6 +193,7 @@ def main(argv=None):
         args.shuffle_seed = box[0]
     rng = random.Random(args.shuffle_seed) if args.shuffle_seed is not None else random
     corpus = None
+    pipe = None
     with ph("ingest"):
         if args.native_ingest:
             files = os.listdir(source_dir)
@@ -200,7 +201,16 @@ def main(argv=None):
             paths = [os.path.join(source_dir, f) for f in files if f.endswith(ending_pattern)]
             print(datetime.datetime.now())
             print(f"native ingest of {len(paths)} files")
-            corpus = ingest.read_corpus(paths)
+            # the shuffles depend only on the pair count and rng: start drawing
+            # the first one (src/gene2vec.py:52) from a newline count while the
+            # files are tokenised
+            n_lines = ingest.count_lines(paths)
+            pipe = ingest.ShufflePipeline(n_lines, rng, max(1, args.iters))
+            try:
+                corpus = ingest.read_corpus(paths)
+            except BaseException:
+                pipe.close(wait=True)
+                raise
             n_pairs = corpus.n_sent
         else:
             gene_pairs = read_gene_pairs(source_dir, ending_pattern, rng)
@@ -211,12 +221,13 @@ def main(argv=None):
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
     exporter = _Exporter(not args.no_txt, not args.no_w2v, args.w2v_binary)
-    pipe = None
     with ph("shuffle"):
         if corpus is not None:
             # this shuffle and the reshuffle before every later iteration (:80)
             # are drawn ahead on host threads while the GPU trains
-            pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
+            if corpus.n_sent != n_lines:  # cannot happen; never shuffle the wrong n
+                pipe.close(wait=True)
+                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
             perm = pipe.next()
             corpus.permute_(perm)
             pipe.release(perm)

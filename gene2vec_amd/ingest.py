@@ -108,6 +108,17 @@ class Corpus:
         return {self.words[i]: int(counts[i]) for i in fo}
 
 
+def count_lines(paths, threads=None):
+    """sentences ``read_corpus(paths)`` will return (g2v_count_lines)"""
+    arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])
+    n = C.c_int64()
+    rc = N.lib().g2v_count_lines(arr, len(paths), threads or min(16, os.cpu_count() or 1),
+                                 C.byref(n))
+    if rc != N.G2V_OK:
+        raise N.G2VError(rc, "g2v_count_lines")
+    return n.value
+
+
 def read_corpus(paths, threads=None):
     L = N.lib()
     arr = (C.c_char_p * len(paths))(*[os.fsencode(p) for p in paths])

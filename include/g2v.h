@@ -324,6 +324,10 @@ int g2v_corpus_export(const g2v_corpus *c, int32_t *tokens, int64_t *sent_off, i
 /* The length every sentence of the corpus has (2 for the pair generator's
  * files: sent_off is then implicit and need not be exported), -1 if ragged. */
 int g2v_corpus_sent_len(const g2v_corpus *c, int64_t *len);
+/* Sentences g2v_corpus_read would return for these files (lines under
+ * universal newlines), from a newline count alone: lets the caller start
+ * drawing src/gene2vec.py:52's shuffle of n pairs before the ingest ends. */
+int g2v_count_lines(const char *const *paths, int n_paths, int n_threads, int64_t *out);
 int g2v_corpus_free(g2v_corpus *c);
 /* out sentence i = in sentence perm[i] (CSR gather) */
 int g2v_csr_permute(const int32_t *tok, const int64_t *off, int64_t n_sent, const int64_t *perm,

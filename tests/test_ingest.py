@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from gene2vec_amd import _native as N
-from gene2vec_amd.ingest import ShufflePipeline, py_shuffle_perm, read_corpus
+from gene2vec_amd.ingest import ShufflePipeline, count_lines, py_shuffle_perm, read_corpus
 
 
 def _py_read(paths):
@@ -58,6 +58,31 @@ def test_native_reader_matches_python(files):
                     words_fo.append(w)
         assert c.words == words_fo
         assert int(c.counts.sum()) == sum(len(s) for s in ref)
+        # the newline count the CLI starts its first shuffle from
+        assert count_lines(files, threads=threads) == len(ref)
+
+
+@pytest.mark.parametrize("text", [b"", b"A B", b"A B\n", b"A B\r\n\r\n", b"\r\r\n\n",
+                                  b"A B\rC D", b"A B\n   ", b"\n", b"A\r", b"A B\r\nC"])
+def test_count_lines_equals_reader(tmp_path, text):
+    """universal newlines at the edges: lone CR, CRLF, unterminated or
+    whitespace-only last line, empty file"""
+    p = tmp_path / "t.txt"
+    p.write_bytes(text)
+    assert count_lines([str(p)], threads=2) == read_corpus([str(p)]).n_sent == len(_py_read([p]))
+
+
+def test_pair_files_keep_offsets_implicit(tmp_path):
+    p = tmp_path / "pairs.txt"
+    p.write_text("A B\nC D\nB A\n")
+    c = read_corpus([str(p)])
+    assert c._sent_off is None and c.pairs_only and c.n_sent == 3
+    np.testing.assert_array_equal(c.sent_off, [0, 2, 4, 6])
+    assert c.sentences() == [["A", "B"], ["C", "D"], ["B", "A"]]
+    q = tmp_path / "ragged.txt"
+    q.write_text("A B\nC\n")
+    r = read_corpus([str(q)])
+    assert r._sent_off is not None and not r.pairs_only
 
 
 def test_undefined_cp1252_byte_raises(tmp_path):
