@@ -441,6 +441,33 @@ def test_striping_keeps_values_exact():
         _close(g1, a1)
 
 
+def test_striped_reads_sum_every_copy():
+    """One chunk (32 examples, one wave, deterministic) over 12 rows, so rows
+    are re-read after their own earlier updates landed in stripe copies: 16
+    copies (two load batches of 7 + one), 3 copies and no striping agree to
+    float rounding of the copy sums."""
+    D, K, B, V = 200, 5, 32, 12
+    rng = np.random.Generator(np.random.PCG64(21))
+    syn0 = ((rng.random((V, D)) - 0.5) / D * 40).astype(np.float32)
+    syn1 = ((rng.random((V, D)) - 0.5) / D * 40).astype(np.float32)
+    center = rng.integers(0, V, B).astype(np.int32)
+    inp = ((center + 1 + rng.integers(0, V - 1, B)) % V).astype(np.int32)
+    negs = rng.integers(0, V, (B, K)).astype(np.int32)
+    outs = []
+    for rows, copies in ((0, 1), (V, 16), (V, 3)):
+        eng = E.SGNSEngine(V, D, K)
+        eng.set_option(N.OPT_STRIPE_ROWS, rows)
+        eng.set_option(N.OPT_STRIPE_COPIES, copies)
+        eng.set_weights(syn0, syn1)
+        eng.step_explicit(center, inp, negs, 0.025, N.MODE_HOGWILD)
+        outs.append(eng.get_weights())
+        eng.close()
+    for g0, g1 in outs[1:]:
+        np.testing.assert_allclose(g0, outs[0][0], rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(g1, outs[0][1], rtol=1e-5, atol=1e-6)
+    assert not np.array_equal(outs[0][1], syn1)
+
+
 def test_sampler_at_c2_full_size_bit_exact():
     """BASELINE C2 at full size (V=24447, 100 M pairs, the bench corpus):
     effective words and directed examples of one production train() equal the
