@@ -24,6 +24,7 @@ average launch time, HIP events on the launch stream) and `cpu_baseline`
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -93,7 +94,9 @@ def parse():
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                         "the N>1 path with several ranks sharing one GPU)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02c.json"))
+    p.add_argument("--traffic-json", default=None,
+                   help="PMC bytes per example for roofline.traffic (default: the "
+                        "profiles/traffic_r02c*.json whose workload matches)")
     return p.parse_args()
 
 
@@ -235,9 +238,13 @@ def main():
     achieved = alg_bytes_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic = None
     traffic_src = None
-    if os.path.exists(a.traffic_json):
+    cands = [a.traffic_json] if a.traffic_json else sorted(
+        glob.glob(os.path.join(ROOT, "profiles", "traffic_r02c*.json")))
+    for tpath in cands:
+        if traffic is not None or not os.path.exists(tpath):
+            continue
         try:
-            tj = json.load(open(a.traffic_json))
+            tj = json.load(open(tpath))
             # per-example PMC bytes of the same workload (vocabulary, shape, downsampling
             # and skew) from a separate rocprofv3 --pmc pass of this kernel, scaled to
             # this run's examples per launch
@@ -245,7 +252,7 @@ def main():
                     tj.get("zipf")) == (V0, D, K, a.sample, a.zipf):
                 traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
                                 * st["examples"] / launches, 1)
-                traffic_src = (f"{os.path.relpath(a.traffic_json, ROOT)}: PMC bytes per "
+                traffic_src = (f"{os.path.relpath(tpath, ROOT)}: PMC bytes per "
                                f"example x this run's {st['examples'] // launches} examples "
                                "per launch (not measured in this process)")
         except Exception:

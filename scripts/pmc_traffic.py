@@ -33,7 +33,7 @@ def bench_line(log):
 
 def main(out):
     c = {}
-    for i in range(1, 6):
+    for i in range(1, 7):
         if os.path.isdir(os.path.join(out, f"p{i}")):
             c.update(counters(os.path.join(out, f"p{i}")))
     b = bench_line(os.path.join(out, "p1.log"))
@@ -59,6 +59,12 @@ def main(out):
         "algorithmic_bytes_per_example": bpe,
         "traffic_over_algorithmic": (fetch + write) / bpe,
     }
+    # requests the L2 sends to the memory controller (DRAM side of the fabric;
+    # MALL hits are not separable from TCC counters on gfx950)
+    if "TCC_EA0_RDREQ_DRAM_sum" in c and c.get("TCC_EA0_RDREQ_sum"):
+        res["ea_rdreq_to_mc_share"] = c["TCC_EA0_RDREQ_DRAM_sum"] / c["TCC_EA0_RDREQ_sum"]
+    if "TCC_EA0_WRREQ_ATOMIC_DRAM_sum" in c and c.get("TCC_EA0_ATOMIC_sum"):
+        res["ea_atomic_to_mc_share"] = c["TCC_EA0_WRREQ_ATOMIC_DRAM_sum"] / c["TCC_EA0_ATOMIC_sum"]
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
               "SQ_INSTS_LDS"):
         if k in c:  # wave-instructions per directed example
