@@ -13,17 +13,20 @@ namespace g2v {
 // ---------------------------------------------------------------------------
 // Same per-example math as k_sgns, but every table update is a memory-side
 // float atomic of the delta (g * syn0[input] into syn1neg[t], lockf * work
-// into syn0[input]).  With ~4k examples in flight on 256 CUs every row of a
+// into syn0[input]).  With thousands of examples in flight every row of a
 // 24k-gene vocabulary is touched every few microseconds, so plain
 // read-modify-write stores lose most updates (measured: iteration-0 loss 4.15
 // vs 2.77 sequential); atomics keep all of them (2.76).
 //
-// Pipelining: example e+1's record and rows are loaded BEFORE example e's
-// atomics are issued, so in the wave's in-order vmcnt they wait only behind
-// example e-1's atomics (the record load's wait drains those; a wave keeps at
-// most one example's atomics in flight).  l1 and work are staged through LDS in element order
+// Pipelining: a wave takes chunks of kChunk consecutive
+// examples from a work queue and stages each chunk's records and lockf in LDS
+// once.  Example e+1's rows are loaded BEFORE example e's atomics are issued
+// and after example e-1's have landed (the wave sees its own updates from two
+// examples back); e's atomics are a fixed number of buffer atomics, so the
+// loop head waits for e+1's rows with vmcnt(#atomics) while e's atomics retire
+// behind e+1's compute.  l1 and work are staged through LDS in element order
 // so each atomic wave-instruction adds 64 contiguous floats (256 B); the
-// D % 64 tails of all K+2 rows are packed into shared instructions.
+// row's buffer resource drops the lanes past D.
 template <int K, int NV>
 struct ExRegs {
   int32_t tg[K + 1];
