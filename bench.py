@@ -77,6 +77,7 @@ def parse():
     p.add_argument("--merge", choices=("touch", "mean"), default="touch",
                    help="replica merge rule (gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
+    p.add_argument("--stripe", default="", help="hot-row stripes ROWSxCOPIES (default: library's)")
     p.add_argument("--seg-jobs", type=int, default=0,
                    help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
@@ -149,6 +150,10 @@ def main():
     eng = E.SGNSEngine(V, D, K, device=local)
     if a.grid:
         eng.set_option(N.OPT_GRID, a.grid)
+    if a.stripe:
+        sr, sc = (int(x) for x in a.stripe.lower().split("x"))
+        eng.set_option(N.OPT_STRIPE_ROWS, sr)
+        eng.set_option(N.OPT_STRIPE_COPIES, sc)
     if a.seg_jobs:
         eng.set_option(N.OPT_SEG_JOBS, a.seg_jobs)
     # a dedicated (non-default) stream: g2v kernels, RCCL all-reduces and the
@@ -269,7 +274,8 @@ def main():
                                     "of added bytes chip-wide)",
                 "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
                 "atomic_frac": round(atomic_gbps / 1300.0, 4), "traffic_source": traffic_src,
-                "grid_workgroups": eng.get_option(N.OPT_GRID)}
+                "grid_workgroups": eng.get_option(N.OPT_GRID),
+                "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}"}
 
     # ---- measured gather roof: the same kernel on the same index
     # stream with its table writes compiled out (G2V_OPT_DEBUG_WRITE=2) and a

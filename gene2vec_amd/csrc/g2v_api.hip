@@ -105,7 +105,7 @@ struct g2v_ctx {
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
-  int stripe_rows = 8, stripe_copies = 8;
+  int stripe_rows = 8, stripe_copies = 0;  // copies 0 = auto (stripe_copies_eff)
   int atomic_overlap = 1;
   float* stripe = nullptr;
   int64_t stripe_cap = 0;
@@ -192,6 +192,18 @@ struct g2v_ctx {
 // 1 workgroup per CU at C2 and ~0.5 at C4, so the budget is set at the
 // quiet end: waves x u_max <= 125 (C2 256 workgroups, C4 117, V 3,000 149).
 constexpr double kStaleBudget = 125.0;
+
+// Copies per striped hot row when G2V_OPT_STRIPE_COPIES is not set.  Every
+// read of a striped row sums its copies (one more load batch on the example's
+// critical path); every copy spreads that row's atomics.  At one workgroup per
+// CU or more the kernel is bound by the memory-side atomics and 16 copies win
+// (C2 266 WGs: 202.6 M ex/s vs 197.2 with 8); below, the grid is held down by
+// the staleness budget, per-example latency binds and 8 win (C2 sample 0 at
+// 162 WGs: 153.6 vs 136.4; C4 at 121: 36.8 vs 36.1).
+static int stripe_copies_eff(const g2v_ctx* c) {
+  if (c->stripe_copies > 0) return c->stripe_copies;
+  return c->sgns_grid >= c->cus ? 16 : 8;
+}
 
 static int default_grid(int cus, int K, int nv, double u_max) {
   int g = std::min(cus * sgns_blocks_per_cu(K, nv), 2 * cus);
@@ -496,8 +508,8 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_rows = (int)value;
       return G2V_OK;
     case G2V_OPT_STRIPE_COPIES:
-      REQUIRE(value >= 1 && value <= 16, G2V_EINVAL, "stripe copies out of [1, 16]");
-      c->stripe_copies = (int)value;
+      REQUIRE(value >= 0 && value <= 16, G2V_EINVAL, "stripe copies out of [0, 16]");
+      c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
       REQUIRE(value >= 0 && value <= 5, G2V_EINVAL, "debug write mode out of [0, 5]");
@@ -526,7 +538,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_GRID: *out = c->sgns_grid; return G2V_OK;
     case G2V_OPT_DEBUG_WRITE: *out = c->debug_write; return G2V_OK;
     case G2V_OPT_STRIPE_ROWS: *out = c->stripe_rows; return G2V_OK;
-    case G2V_OPT_STRIPE_COPIES: *out = c->stripe_copies; return G2V_OK;
+    case G2V_OPT_STRIPE_COPIES: *out = stripe_copies_eff(c); return G2V_OK;
     case G2V_OPT_ATOMIC_OVERLAP: *out = c->atomic_overlap; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
@@ -857,14 +869,14 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.loss_f64 = c->d_loss;
   s.loss_f32 = reinterpret_cast<float*>(c->d_loss + 1);
   const bool atomic_kernel = mode == kModeHogwild && s.hot_rows >= c->V;
+  const int copies = stripe_copies_eff(c);
   // rows past what a 1 GiB stripe buffer holds stay unstriped (kStripeMaxBytes)
   const int64_t max_rows =
-      c->stripe_copies > 1 ? kStripeMaxBytes / (2 * 4 * (int64_t)(c->stripe_copies - 1) * c->ld)
-                           : 0;
+      copies > 1 ? kStripeMaxBytes / (2 * 4 * (int64_t)(copies - 1) * c->ld) : 0;
   const int srows = (int)std::min<int64_t>(std::min(c->stripe_rows, c->V), max_rows);
-  const bool striped = atomic_kernel && c->stripe_copies > 1 && srows > 0;
+  const bool striped = atomic_kernel && copies > 1 && srows > 0;
   s.stripe_rows = striped ? srows : 0;
-  s.stripe_copies = striped ? c->stripe_copies : 1;
+  s.stripe_copies = striped ? copies : 1;
   s.overlap = c->atomic_overlap;
   s.queue = c->d_queue;
   int rc;

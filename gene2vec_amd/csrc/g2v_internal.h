@@ -29,6 +29,12 @@ constexpr int kSampleThreads = 1024;
 // k_sgns_atomic addresses the stripe buffer with 32-bit buffer offsets and
 // masks unused copies with an offset past it: the buffer stays below 1 GiB
 constexpr int64_t kStripeMaxBytes = 1ll << 30;
+// stripe buffer layout [table][hot row][copy 1..copies-1][ld]: the copies of
+// one row are adjacent (spread over consecutive lines / channels, read as one
+// contiguous run); row index of copy c of row t of table tbl
+__host__ __device__ inline int64_t stripe_row(int tbl, int t, int c, int rows, int copies) {
+  return ((int64_t)tbl * rows + t) * (copies - 1) + (c - 1);
+}
 constexpr int kSgnsThreads = 256;
 constexpr int kChunk = 32;  // consecutive examples a wave trains per grid-stride step
 

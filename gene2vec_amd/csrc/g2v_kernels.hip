@@ -334,7 +334,7 @@ __global__ void k_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
   float4 acc = *m;
   for (int c = 1; c < copies; ++c) {
     float4* p = reinterpret_cast<float4*>(
-                    stripe + (((int64_t)tbl * (copies - 1) + (c - 1)) * rows + t) * ld) + col;
+                    stripe + stripe_row(tbl, t, c, rows, copies) * ld) + col;
     const float4 q = *p;
     acc.x += q.x;
     acc.y += q.y;

@@ -63,7 +63,8 @@ __device__ __forceinline__ void add_stripes(float4 (&o)[NV], const SgnsArgs& a,
 #pragma unroll
     for (int j = 0; j < kStripeBatch; ++j) {
       const int c = c0 + j;
-      const int base = c < C ? ((tbl * (C - 1) + (c - 1)) * a.stripe_rows + t) * rowb : kStripeOob;
+      const int base =
+          c < C ? (int)stripe_row(tbl, t, c, a.stripe_rows, C) * rowb : kStripeOob;
 #pragma unroll
       for (int v = 0; v < NV; ++v)
         q[j][v] = on[v] ? bload4<0>(rs, base + lane * 16 + 1024 * v)
@@ -93,7 +94,7 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
     return reinterpret_cast<float*>(a.dbg16) + (tbl * nrow + rr) * a.ld;
   }
   if (c == 0 || t >= a.stripe_rows) return (tbl ? a.wr1 : a.wr0) + (int64_t)t * a.ld;
-  return a.stripe + (((int64_t)tbl * (a.stripe_copies - 1) + (c - 1)) * a.stripe_rows + t) * a.ld;
+  return a.stripe + stripe_row(tbl, t, c, a.stripe_rows, a.stripe_copies) * a.ld;
 }
 
 // record e of the chunk staged in LDS (k_sgns_atomic stages each chunk's

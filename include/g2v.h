@@ -116,8 +116,10 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         atomics into a scratch table, 5 syn1neg atomics only
  *                         (syn0 never written) [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
- *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off [8] (values stay exact:
- *                         readers sum the copies, each launch folds them back)
+ *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off, 0 = auto: 16 when the
+ *                         SGNS grid fills every CU, 8 below [0] (values stay
+ *                         exact: readers sum the copies, each launch folds them
+ *                         back; g2v_get_option reads the value in use)
  *   G2V_OPT_ATOMIC_OVERLAP Hogwild kernel: 1 = a wave's table atomics retire
  *                         behind its next example's compute, 0 = they land
  *                         before it (less staleness per wave, more waves
