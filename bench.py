@@ -96,8 +96,8 @@ def parse():
                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                         "the N>1 path with several ranks sharing one GPU)")
     p.add_argument("--traffic-json", default=None,
-                   help="PMC bytes per example for roofline.traffic (default: the "
-                        "profiles/traffic_r02c*.json whose workload matches)")
+                   help="PMC bytes per example for roofline.traffic (default: the newest "
+                        "profiles/traffic_r*.json whose workload matches)")
     return p.parse_args()
 
 
@@ -243,8 +243,9 @@ def main():
     achieved = alg_bytes_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic = None
     traffic_src = None
+    # the newest profile of this workload (traffic_<round tag>[_<config>].json)
     cands = [a.traffic_json] if a.traffic_json else sorted(
-        glob.glob(os.path.join(ROOT, "profiles", "traffic_r02c*.json")))
+        glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")), reverse=True)
     for tpath in cands:
         if traffic is not None or not os.path.exists(tpath):
             continue
