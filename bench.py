@@ -211,10 +211,15 @@ def main():
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    # per-step events on the same stream (SURVEY 8(d) asks for the median step
+    # as well); value stays whole-job throughput over the bracketed region
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
     w0 = time.perf_counter()
     ev0.record(stream)
     for i in range(a.steps):
+        marks[i].record(stream)
         step(a.warmup + i, True)
+    marks[a.steps].record(stream)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -222,6 +227,7 @@ def main():
     wall = time.perf_counter() - w0
     st = eng.read_stats()
     gpu_ms = ev0.elapsed_time(ev1)
+    step_ms = [round(marks[i].elapsed_time(marks[i + 1]), 3) for i in range(a.steps)]
     elapsed = max(wall, gpu_ms / 1e3)
     if world > 1:
         el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -376,6 +382,7 @@ def main():
             "merge": ({"backend": merge_backend, "rule": a.merge, "every_jobs": avg_every,
                        "merges": trainer.averages, "note": merge_note} if world > 1 else None),
             "gpu_event_ms": round(gpu_ms, 3), "wall_s": round(wall, 4),
+            "step_ms_rank0": step_ms, "step_ms_median_rank0": float(np.median(step_ms)),
             "corpus_gen_s": round(t_corpus, 2),
         }
         print(json.dumps(out), flush=True)
