@@ -38,13 +38,17 @@ struct ExRegs {
 
 // row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
 // the main row ...
+// Lanes past D read through an out-of-range offset (loff = kLaneOob): the
+// buffer range check returns zeros without a memory access, so the loads
+// need no exec-masked branch.  Every table is below 2 GiB (g2v_create) and
+// the stripe buffer below 1 GiB, so row offset + kLaneOob never wraps.
+constexpr uint32_t kLaneOob = 0x80000000u;
 template <int NV>
 __device__ __forceinline__ void load_main(float4 (&o)[NV], __amdgpu_buffer_rsrc_t rmain, int t,
-                                          int rowb, int lane, const bool (&on)[NV]) {
-  const int off = t * rowb + lane * 16;
+                                          int rowb, const uint32_t (&loff)[NV]) {
+  const uint32_t off = (uint32_t)(t * rowb);
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
-    o[v] = on[v] ? bload4<0>(rmain, off + 1024 * v) : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int v = 0; v < NV; ++v) o[v] = bload4<0>(rmain, (int)(off + loff[v]));
 }
 
 // ... plus its stripe copies when t is a striped hot row (t < stripe_rows).
@@ -56,19 +60,18 @@ constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run
 template <int NV>
 __device__ __forceinline__ void add_stripes(float4 (&o)[NV], const SgnsArgs& a,
                                             __amdgpu_buffer_rsrc_t rs, int t, int tbl, int rowb,
-                                            int lane, const bool (&on)[NV]) {
+                                            const uint32_t (&loff)[NV]) {
   const int C = a.stripe_copies;
   for (int c0 = 1; c0 < C; c0 += kStripeBatch) {
     float4 q[kStripeBatch][NV];
 #pragma unroll
     for (int j = 0; j < kStripeBatch; ++j) {
       const int c = c0 + j;
-      const int base =
-          c < C ? (int)stripe_row(tbl, t, c, a.stripe_rows, C) * rowb : kStripeOob;
+      const uint32_t base =
+          c < C ? (uint32_t)((int)stripe_row(tbl, t, c, a.stripe_rows, C) * rowb)
+                : (uint32_t)kStripeOob;
 #pragma unroll
-      for (int v = 0; v < NV; ++v)
-        q[j][v] = on[v] ? bload4<0>(rs, base + lane * 16 + 1024 * v)
-                        : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int v = 0; v < NV; ++v) q[j][v] = bload4<0>(rs, (int)(base + loff[v]));
     }
 #pragma unroll
     for (int j = 0; j < kStripeBatch; ++j) {
@@ -85,16 +88,22 @@ __device__ __forceinline__ void add_stripes(float4 (&o)[NV], const SgnsArgs& a,
 
 // destination of an atomic delta for row t of table tbl: main or stripe copy c
 // (WR 4, ablation: the same rows of a scratch table the kernel never reads)
+// Byte offsets in 32 bits: g2v_create caps a table below 2 GiB (the buffer
+// offset range) and the stripe buffer below 1 GiB, so a row's offset is one
+// scalar multiply.
 template <int WR = 0>
-__device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int c) {
+__device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int c, int rowb) {
   if (WR == 4) {
     const int64_t nrow = (int64_t)a.V + (int64_t)(a.stripe_copies - 1) * a.stripe_rows;
     const int64_t rr =
         (c == 0 || t >= a.stripe_rows) ? t : a.V + (int64_t)(c - 1) * a.stripe_rows + t;
     return reinterpret_cast<float*>(a.dbg16) + (tbl * nrow + rr) * a.ld;
   }
-  if (c == 0 || t >= a.stripe_rows) return (tbl ? a.wr1 : a.wr0) + (int64_t)t * a.ld;
-  return a.stripe + stripe_row(tbl, t, c, a.stripe_rows, a.stripe_copies) * a.ld;
+  if (c == 0 || t >= a.stripe_rows)
+    return reinterpret_cast<float*>(reinterpret_cast<char*>(tbl ? a.wr1 : a.wr0) +
+                                    (uint32_t)(t * rowb));
+  const int sr = (tbl * a.stripe_rows + t) * (a.stripe_copies - 1) + (c - 1);  // stripe_row()
+  return reinterpret_cast<float*>(reinterpret_cast<char*>(a.stripe) + (uint32_t)(sr * rowb));
 }
 
 // record e of the chunk staged in LDS (k_sgns_atomic stages each chunk's
@@ -104,27 +113,27 @@ template <int K, int NV>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
                                              const int32_t* r, __amdgpu_buffer_rsrc_t r0,
                                              __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
-                                             int rowb, int lane, const bool (&on)[NV]) {
+                                             int rowb, const uint32_t (&loff)[NV]) {
   x.tg[0] = __builtin_amdgcn_readfirstlane(r[0]);
   x.input = __builtin_amdgcn_readfirstlane(r[1]);
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
 #pragma unroll
   for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
-  load_main<NV>(x.l1, r0, x.input, rowb, lane, on);
+  load_main<NV>(x.l1, r0, x.input, rowb, loff);
 #pragma unroll
   for (int d = 0; d <= K; ++d) {
     if (x.tg[d] >= 0) {
-      load_main<NV>(x.rw[d], r1, x.tg[d], rowb, lane, on);
+      load_main<NV>(x.rw[d], r1, x.tg[d], rowb, loff);
     } else {
 #pragma unroll
       for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  if (x.input < a.stripe_rows) add_stripes<NV>(x.l1, a, rs, x.input, 0, rowb, lane, on);
+  if (x.input < a.stripe_rows) add_stripes<NV>(x.l1, a, rs, x.input, 0, rowb, loff);
 #pragma unroll
   for (int d = 0; d <= K; ++d)
     if (x.tg[d] >= 0 && x.tg[d] < a.stripe_rows)
-      add_stripes<NV>(x.rw[d], a, rs, x.tg[d], 1, rowb, lane, on);
+      add_stripes<NV>(x.rw[d], a, rs, x.tg[d], 1, rowb, loff);
 }
 
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
@@ -171,6 +180,22 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 // and apply early, high-alpha examples to a model the others have already
 // moved on: C2 vocabulary at 266 workgroups drifted +0.42 % from the
 // sequential objective, 256 and 300 stayed within 0.1 %.
+// a value every lane holds alike (a wave_allreduce_d total) as a scalar: the
+// compiler cannot prove the butterfly's result uniform, and a branch on it
+// would turn every later row choice into exec-masked VALU work (round 2: ~55
+// instructions per row update, most of them address arithmetic)
+__device__ __forceinline__ float uniform_f(float x) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+
+// (c mod C) for 0 <= c < C + 32: the stripe copy of a row update without an
+// integer division per row
+__device__ __forceinline__ int wrap_copy(int c, int C) {
+  if (C == 1) return 0;
+  while (c >= C) c -= C;
+  return c;
+}
+
 __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
   unsigned int v = 0;
   if (lane == 0) v = atomicAdd(q, 1u);
@@ -208,9 +233,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   float* sw = s_wk[wid];
   int32_t* sr = s_rec[wid];
   float* slf = s_lf[wid];
-  bool on[NV];
+  uint32_t loff[NV];  // this lane's byte offset in a row, out of range past D
 #pragma unroll
-  for (int v = 0; v < NV; ++v) on[v] = (lane + 64 * v) < a.nvec;
+  for (int v = 0; v < NV; ++v)
+    loff[v] = (lane + 64 * v) < a.nvec ? (uint32_t)(lane * 16 + 1024 * v) : kLaneOob;
 
   for (int64_t c = next_chunk(a.queue, lane); c * kChunk < E; c = next_chunk(a.queue, lane)) {
     const int64_t e_beg = c * kChunk;
@@ -225,10 +251,12 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       if (lane < e_end - e_beg) slf[lane] = a.lockf[sr[lane * RS + 1]];
       __builtin_amdgcn_wave_barrier();
     }
-    const int cb0 = (int)(e_beg % (int64_t)a.stripe_copies);
+    // stripe copy of example e's first row update: (e + d) mod copies, advanced
+    // per example (no division in the loop)
+    int cbase = (int)(e_beg % (int64_t)a.stripe_copies);
     float lsum = 0.f;
     ExRegs<K, NV> x;
-    load_example<K, NV>(x, a, sr, r0, r1, rs, rowb, lane, on);
+    load_example<K, NV>(x, a, sr, r0, r1, rs, rowb, loff);
     // drain here, so the loop head only waits on the back edge's count
     // (vmcnt(#atomics of the previous example)); without it the two incoming
     // paths merge to vmcnt(0), which also waits for the previous atomics
@@ -255,7 +283,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       float fv[NT], lv[NT], lg[NT];
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
-        fv[d] = (float)dot[d];
+        fv[d] = uniform_f((float)dot[d]);
         const bool in = fv[d] > -(float)kMaxExp && fv[d] < (float)kMaxExp;
         lv[d] = s_lut[in ? (int)((fv[d] + (float)kMaxExp) * (float)kLutScale) : 0];
         if (LOSS) {
@@ -287,7 +315,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           double s = 0.0;
 #pragma unroll
           for (int v = 0; v < NV; ++v) s = dot4(x.l1[v], x.rw[d][v], s);
-          f = (float)wave_allreduce_d(s);
+          f = uniform_f((float)wave_allreduce_d(s));
           dirty[d] = true;
           if (f > -(float)kMaxExp && f < (float)kMaxExp) {
             lut = s_lut[(int)((f + (float)kMaxExp) * (float)kLutScale)];
@@ -342,10 +370,9 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       // before this pipelining: the Hogwild staleness stays what the grid
       // budget was measured with)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rowb, lane, on);
+      if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rowb, loff);
 
       // ---- atomics of example e -----------------------------------------------
-      const int cbase = (cb0 + q) % a.stripe_copies;
       if (WR == 3) {
         typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
         const int hw = (int)(a.ld >> 1);
@@ -371,16 +398,18 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           }
         }
         __builtin_amdgcn_wave_barrier();
+        cbase = cbase + 1 == a.stripe_copies ? 0 : cbase + 1;
         continue;
       }
       // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work
 #pragma unroll
       for (int d = 0; d < NT; ++d)
-        emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, (cbase + d) % a.stripe_copies),
+        emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, wrap_copy(cbase + d, a.stripe_copies), rowb),
                          live[d], D, v1, g[d], lane);
-      emit_row<NV, WR>(upd_row<WR>(a, 0, input, (cbase + NT) % a.stripe_copies),
+      emit_row<NV, WR>(upd_row<WR>(a, 0, input, wrap_copy(cbase + NT, a.stripe_copies), rowb),
                        any && WR != 5, D, vw, lf, lane);
       __builtin_amdgcn_wave_barrier();
+      cbase = cbase + 1 == a.stripe_copies ? 0 : cbase + 1;
     }
     if (LOSS && lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);
   }
