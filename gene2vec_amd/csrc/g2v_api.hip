@@ -1106,6 +1106,22 @@ int g2v_cosine_pairs(int device, const float* vectors, int64_t V, int32_t D, con
   return G2V_OK;
 }
 
+int g2v_permute_items8(int device, const void* src, void* dst, int64_t n_items, int64_t first,
+                       int64_t count, uint64_t seed, void* stream) {
+  REQUIRE(n_items >= 0 && first >= 0 && count >= 0 && first <= n_items &&
+              count <= n_items - first,
+          G2V_EINVAL, "positions [%lld, %lld) outside the %lld items", (long long)first,
+          (long long)(first + count), (long long)n_items);
+  REQUIRE(count == 0 || (src && dst), G2V_EINVAL, "null device pointer");
+  REQUIRE(n_items < (1ll << 62), G2V_ERANGE, "%lld items: at most 2^62", (long long)n_items);
+  if (count == 0) return G2V_OK;
+  HIPCHK(hipSetDevice(device));
+  const PermKey pk = perm_key((uint64_t)n_items, seed);
+  HIPCHK(launch_permute8(static_cast<const uint64_t*>(src), static_cast<uint64_t*>(dst), pk, first,
+                         count, static_cast<hipStream_t>(stream)));
+  return G2V_OK;
+}
+
 int g2v_sync(g2v_ctx* c) {
   int rc = set_dev(c);
   if (rc) return rc;

@@ -150,6 +150,48 @@ hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t
                               int rule, hipStream_t st);
 hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const int32_t* a,
                                const int32_t* b, int64_t n, float* out, hipStream_t st);
+// Keyed pseudo-random permutation of [0, n) (the device reshuffle of the
+// pair corpus, g2v_permute_items8): a 6-round balanced Feistel network on 2h
+// bits (4^h >= n) with splitmix64-finalizer round functions, cycle-walked
+// into [0, n).  Restated in oracle/shuffle_oracle.py.
+struct PermKey {
+  uint64_t k[6];
+  uint64_t n;
+  int half;  // h
+};
+__host__ __device__ inline uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xbf58476d1ce4e5b9ull;
+  z ^= z >> 27;
+  z *= 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  return z;
+}
+inline PermKey perm_key(uint64_t n, uint64_t seed) {
+  PermKey pk{};
+  pk.n = n;
+  pk.half = 1;
+  while (pk.half < 31 && (1ull << (2 * pk.half)) < n) ++pk.half;
+  for (int r = 0; r < 6; ++r) pk.k[r] = mix64(seed + 0x9e3779b97f4a7c15ull * (uint64_t)(r + 1));
+  return pk;
+}
+__host__ __device__ inline uint64_t perm_at(const PermKey& pk, uint64_t i) {
+  const uint64_t mask = (1ull << pk.half) - 1;
+  uint64_t y = i;
+  do {
+    uint64_t L = y >> pk.half, R = y & mask;
+#pragma unroll
+    for (int r = 0; r < 6; ++r) {
+      const uint64_t t = L ^ (mix64(R ^ pk.k[r]) & mask);
+      L = R;
+      R = t;
+    }
+    y = (L << pk.half) | R;
+  } while (y >= pk.n);
+  return y;
+}
+hipError_t launch_permute8(const uint64_t* src, uint64_t* dst, const PermKey& pk, int64_t first,
+                           int64_t count, hipStream_t st);
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
                         double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
                         hipStream_t st);

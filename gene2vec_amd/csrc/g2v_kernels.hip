@@ -23,6 +23,8 @@
 //
 // Everything is memory-gather bound (0.68 flop/B): no MFMA by design.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "g2v_device.h"
@@ -536,6 +538,25 @@ hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const
   if (n > 0)
     hipLaunchKernelGGL(k_pair_dot, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, st, u, D, a, b, n,
                        out);
+  return hipGetLastError();
+}
+
+// dst[i] = src[perm(first + i)], 8-byte items (an int32 gene pair): the
+// per-iteration reshuffle of a device-resident pair corpus, each rank
+// gathering only its own shard of the permuted order
+__global__ void k_permute8(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, PermKey pk,
+                           int64_t first, int64_t count) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride)
+    dst[i] = src[perm_at(pk, (uint64_t)(first + i))];
+}
+
+hipError_t launch_permute8(const uint64_t* src, uint64_t* dst, const PermKey& pk, int64_t first,
+                           int64_t count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  const int64_t blocks = std::min<int64_t>((count + 255) / 256, 16384);
+  hipLaunchKernelGGL(k_permute8, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, pk, first,
+                     count);
   return hipGetLastError();
 }
 

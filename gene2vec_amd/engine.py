@@ -70,6 +70,17 @@ def seeded_vectors(seeds, dim):
     return out
 
 
+def permute_items8(device, src_ptr, dst_ptr, n_items, first, count, seed, stream=None):
+    """g2v_permute_items8: dst[i] = src[p(first + i)] for a device-resident
+    corpus of 8-byte items (int32 pairs), p a keyed permutation of [0, n_items)
+    (the per-iteration reshuffle of src/gene2vec.py:80 done in HBM).  Enqueued
+    on ``stream`` (a HIP stream handle, None = null stream)."""
+    N.check(N.lib().g2v_permute_items8(int(device), C.c_void_p(src_ptr), C.c_void_p(dst_ptr),
+                                       int(n_items), int(first), int(count),
+                                       int(seed) % 2 ** 64,
+                                       C.c_void_p(stream) if stream else None))
+
+
 def count_ids(ids, V):
     ids = np.ascontiguousarray(ids, dtype=np.int32)
     counts = np.zeros(V, dtype=np.int64)

@@ -28,6 +28,7 @@ import time
 
 import numpy as np
 
+from . import engine as E
 from . import generateMatrix as gM
 from . import ingest
 from .word2vec import Word2Vec
@@ -91,6 +92,46 @@ def _sentences(corpus, pairs_only):
     """train_ids' sentence layout: (None, 2) for an all-pairs corpus (same jobs
     and sampled stream as its CSR form), else the CSR offsets"""
     return (None, 2) if pairs_only else (corpus.sent_off, 0)
+
+
+class _DeviceOrder:
+    """``--shuffle device``: the pair corpus stays in HBM in the order of the
+    first shuffle (src/gene2vec.py:52, CPython-exact: it fixes the vocabulary
+    order); every later reshuffle (:80, an unseeded random.shuffle in the
+    reference, so any uniform permutation is as faithful) is a keyed
+    permutation of that order evaluated on the GPU, each data-parallel rank
+    gathering only its own shard (g2v_permute_items8).  Replaces a serial
+    host Fisher-Yates over the whole corpus on every rank and the per-iteration
+    host-to-device copy of the tokens."""
+
+    def __init__(self, tok, ids, device, rank, world):
+        import torch
+        from . import distributed as Dd
+        self.torch = torch
+        self.device = device
+        self.dev = torch.device("cuda", device)
+        self.ids = ids
+        flat = np.ascontiguousarray(tok, dtype=np.int32)
+        self.base = torch.from_numpy(flat.view(np.int64)).to(self.dev)  # one pair per item
+        self.n = self.base.numel()
+        self.s0, self.s1 = Dd.shard_range(self.n, rank, world)
+        self.buf = None
+
+    def shard(self, seed):
+        """(ptr, n_tokens, keepalive) of this rank's pairs; seed None = the
+        first-shuffle order itself (iteration 1)"""
+        torch = self.torch
+        if seed is None:
+            t = self.base[self.s0:self.s1]
+        else:
+            if self.buf is None:
+                self.buf = torch.empty(self.s1 - self.s0, dtype=torch.int64, device=self.dev)
+            st = torch.cuda.current_stream(self.dev)
+            E.permute_items8(self.device, self.base.data_ptr(), self.buf.data_ptr(), self.n,
+                             self.s0, self.s1 - self.s0, seed, st.cuda_stream)
+            st.synchronize()  # the engine reads it on its own stream
+            t = self.buf
+        return t.data_ptr(), 2 * t.numel(), t
 
 
 class _Exporter:
@@ -178,8 +219,16 @@ def main(argv=None):
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
     parser.add_argument("--merge-every-jobs", type=int, default=1024,
                         help="data-parallel replica merge cadence (gensim jobs per rank)")
+    parser.add_argument("--shuffle", choices=("python", "device"), default=None,
+                        help="reshuffles before iterations >= 2 (src/gene2vec.py:80): 'python' = "
+                             "CPython's random.shuffle bit for bit on the host; 'device' = a "
+                             "keyed permutation of the HBM-resident pairs on the GPU (needs "
+                             "--native-ingest and a pairs-only corpus; default under torchrun)")
     args = parser.parse_args(argv)
     rank, world = _init_dp(args)
+    # data-parallel ranks would each redo a serial Fisher-Yates over the whole
+    # corpus per iteration: reshuffle on the device instead unless asked
+    shuffle_mode = args.shuffle or ("device" if world > 1 else "python")
     ph = _Phases()
     source_dir, export_dir, ending_pattern = args.fileAddress[:3]
 
@@ -205,7 +254,8 @@ def main(argv=None):
             # the first one (src/gene2vec.py:52) from a newline count while the
             # files are tokenised
             n_lines = ingest.count_lines(paths)
-            pipe = ingest.ShufflePipeline(n_lines, rng, max(1, args.iters))
+            n_shuffles = 1 if shuffle_mode == "device" else max(1, args.iters)
+            pipe = ingest.ShufflePipeline(n_lines, rng, n_shuffles)
             try:
                 corpus = ingest.read_corpus(paths)
             except BaseException:
@@ -218,6 +268,11 @@ def main(argv=None):
         # every line a pair (the generator's output): fixed-length sentences,
         # no 8-byte offsets per pair to upload; shuffles keep the lengths
         pairs_only = corpus is not None and corpus.pairs_only
+    if shuffle_mode == "device" and not pairs_only:
+        print("--shuffle device needs --native-ingest and a pairs-only corpus: "
+              "using Python's shuffle")
+        shuffle_mode = "python"
+    dorder = None
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
     exporter = _Exporter(not args.no_txt, not args.no_w2v, args.w2v_binary)
@@ -227,10 +282,14 @@ def main(argv=None):
             # are drawn ahead on host threads while the GPU trains
             if corpus.n_sent != n_lines:  # cannot happen; never shuffle the wrong n
                 pipe.close(wait=True)
-                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
+                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, n_shuffles)
             perm = pipe.next()
             corpus.permute_(perm)
             pipe.release(perm)
+            if shuffle_mode == "python" and n_shuffles == 1 and args.iters > 1:
+                # fell back from --shuffle device: draw the later reshuffles too
+                pipe.close(wait=True)
+                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, args.iters - 1)
         else:
             rng.shuffle(gene_pairs)
     print(datetime.datetime.now())
@@ -264,13 +323,24 @@ def main(argv=None):
                         tok = ids[corpus.tokens]
                         _adopt_vocab_ids(corpus, ids, tok)
                     with ph("train"):
-                        model.train_ids(tok, *_sentences(corpus, pairs_only),
-                                        total_examples=model.corpus_count, epochs=model.iter)
+                        if shuffle_mode == "device":
+                            dorder = _DeviceOrder(tok, _vocab_ids(model, corpus), args.device,
+                                                  rank, world)
+                            model.train_ids(None, None, 2, total_examples=model.corpus_count,
+                                            epochs=model.iter, device_tokens=dorder.shard(None))
+                        else:
+                            model.train_ids(tok, *_sentences(corpus, pairs_only),
+                                            total_examples=model.corpus_count,
+                                            epochs=model.iter)
             else:
                 print(datetime.datetime.now())
                 print("shuffle start " + str(n_pairs))
                 with ph("shuffle"):
-                    if corpus is not None:
+                    if shuffle_mode == "device":
+                        # same draw on every rank (one seed, src/gene2vec.py:80's
+                        # random.shuffle is the reference's); applied on the device
+                        perm_seed = rng.getrandbits(64)
+                    elif corpus is not None:
                         perm = pipe.next()
                         corpus.permute_(perm)
                         pipe.release(perm)
@@ -299,9 +369,20 @@ def main(argv=None):
                             tok = corpus.tokens  # adopted at iteration 1: ids are the model's
                         else:
                             tok = ids[corpus.tokens]
+                        if dorder is not None and not np.array_equal(ids, dorder.ids):
+                            # another vocabulary numbering: the resident order is
+                            # re-uploaded (the model keeps its vocabulary, so never
+                            # in the reference's loop)
+                            dorder = _DeviceOrder(tok, ids, args.device, rank, world)
                     with ph("train"):
-                        model.train_ids(tok, *_sentences(corpus, pairs_only),
-                                        total_examples=model.corpus_count, epochs=model.iter)
+                        if dorder is not None:
+                            model.train_ids(None, None, 2, total_examples=model.corpus_count,
+                                            epochs=model.iter,
+                                            device_tokens=dorder.shard(perm_seed))
+                        else:
+                            model.train_ids(tok, *_sentences(corpus, pairs_only),
+                                            total_examples=model.corpus_count,
+                                            epochs=model.iter)
             with ph("save"):
                 model._sync_host()
                 if rank == 0:  # data parallel: the merged replicas are identical

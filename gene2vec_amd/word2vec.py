@@ -539,9 +539,15 @@ class Word2Vec:
 
     def train_ids(self, tokens, sent_off=None, sent_len=0, total_examples=None,
                   total_words=None, epochs=1, start_alpha=None, end_alpha=None,
-                  compute_loss=False):
+                  compute_loss=False, device_tokens=None):
         """Fast path: pre-tokenised corpus (int32 vocabulary indices, -1 = OOV)
-        as CSR sentence offsets or fixed-length sentences (pairs: sent_len=2)."""
+        as CSR sentence offsets or fixed-length sentences (pairs: sent_len=2).
+
+        ``device_tokens = (ptr, n_tokens, keepalive)``: the pairs already sit
+        in this GPU's memory (``tokens`` is then ignored, sent_len must be 2)
+        and, under data parallelism, are already this rank's shard (the CLI's
+        ``--shuffle device`` gathers each rank's shard of the reshuffled order
+        on the device, g2v_permute_items8)."""
         self.alpha = float(start_alpha or self.alpha)
         self.min_alpha = float(end_alpha or self.min_alpha)
         self.epochs = epochs
@@ -552,7 +558,12 @@ class Word2Vec:
         eng = self._ensure_engine()
         eng.reset_loss()
         rank, world = self._dp_world()
-        if world > 1:
+        if device_tokens is not None:
+            if sent_len != 2:
+                raise ValueError("device_tokens carry fixed-length pairs (sent_len=2)")
+            if world > 1:
+                total_examples, total_words = device_tokens[1] // 2, None
+        elif world > 1:
             # contiguous shard of the (shuffled) sentences per rank; alpha follows
             # the shard's own progress, which is the global progress (all ranks
             # advance together)
@@ -565,7 +576,13 @@ class Word2Vec:
                 tokens = tokens[so[s0]:so[s1]]
                 sent_off = so[s0:s1 + 1] - so[s0]
             total_examples, total_words = s1 - s0, None
-        if sent_len > 0:
+        if device_tokens is not None:
+            ptr, n_tok, keep = device_tokens
+            n_sent = n_tok // 2
+            eng.set_corpus_device(ptr, n_tok, sent_len=2, keepalive=keep)
+            js = E.plan_jobs(n_sent=n_sent, sent_len=2)
+            lengths_total = n_tok
+        elif sent_len > 0:
             n_sent = len(tokens) // sent_len
             eng.set_corpus(tokens, sent_len=sent_len)
             js = E.plan_jobs(n_sent=n_sent, sent_len=sent_len)

@@ -302,6 +302,20 @@ int g2v_coexpr_last_timing(double *mask_ms, double *total_ms);
 int g2v_cosine_pairs(int device, const float *vectors, int64_t V, int32_t D, const int32_t *a,
                      const int32_t *b, int64_t n, float *out);
 
+/* ---- device reshuffle of a pair corpus ------------------------------------------- */
+/* The per-iteration reshuffle of src/gene2vec.py:80 (random.shuffle, unseeded
+ * there) for a corpus resident in HBM: dst[i] = src[p(first + i)] for i < count,
+ * where p is a keyed pseudo-random permutation of [0, n_items) (6-round Feistel
+ * on 2h bits, 4^h >= n_items, splitmix64 round functions, cycle-walking; the
+ * same seed gives the same p on every device, so data-parallel ranks gather
+ * disjoint shards of one permutation).  Not CPython's shuffle: the reference
+ * leaves its shuffles unseeded, so any uniform permutation is as faithful;
+ * g2v_py_shuffle* keep the bit-exact host form.  src holds n_items 8-byte items
+ * (one int32 pair each), dst count items, both device memory of `device`;
+ * enqueued on `stream` (NULL: the null stream), no synchronisation. */
+int g2v_permute_items8(int device, const void *src, void *dst, int64_t n_items, int64_t first,
+                       int64_t count, uint64_t seed, void *stream);
+
 /* ---- host-native helpers (no device work) -------------------------------------- */
 /* [ext] Word2VecTrainables.seeded_vector for every row: row i =
  * (RandomState(seeds[i]).rand(D) - 0.5) / D as float32, seeds[i] =

@@ -45,6 +45,8 @@ def main():
     p.add_argument("--iters", type=int, default=10)
     p.add_argument("--vocab", type=int, default=24447)
     p.add_argument("--keep", action="store_true")
+    p.add_argument("--shuffle", choices=("python", "device"), default="python",
+                   help="the CLI's --shuffle (reshuffles of iterations >= 2)")
     a = p.parse_args()
     work = tempfile.mkdtemp(prefix="g2v_e2e_")
     data, out = os.path.join(work, "data"), os.path.join(work, "out")
@@ -56,13 +58,13 @@ def main():
     t = time.perf_counter()
     with contextlib.redirect_stdout(log):
         outs = G.main([data, out, "txt", "--native-ingest", "--hash", "crc32",
-                       "--shuffle-seed", "7", "--iters", str(a.iters),
+                       "--shuffle-seed", "7", "--iters", str(a.iters), "--shuffle", a.shuffle,
                        "--timing", os.path.join(work, "phases.json")])
     total = time.perf_counter() - t
     sizes = {os.path.basename(f): os.path.getsize(f) for f in
              [outs[-1] + ".txt", outs[-1] + "_w2v.txt"]}
     res = {"metric": "gene2vec CLI end to end (native ingest + %d iterations + exports)" % a.iters,
-           "pairs": a.pairs, "files": a.files, "wall_s": round(total, 2),
+           "pairs": a.pairs, "files": a.files, "shuffle": a.shuffle, "wall_s": round(total, 2),
            "pairs_per_s_incl_io": round(a.pairs * a.iters / total, 1),
            "corpus_write_s_excluded": round(t_write, 2), "outputs": sizes,
            "phases_s": json.load(open(os.path.join(work, "phases.json")))}

@@ -1,0 +1,72 @@
+"""GPU: g2v_permute_items8, the device reshuffle of a pair corpus resident in
+HBM (src/gene2vec.py:80's per-iteration random.shuffle, for the CLI's
+``--shuffle device`` and the data-parallel ranks): bit for bit the restated
+permutation (oracle/shuffle_oracle.py) at small sizes and ragged shards, and
+a permutation of the whole corpus at the C2 size (100 M pairs) and for 8
+data-parallel shards of C3's per-node order (sizes scaled to one GPU)."""
+import numpy as np
+import pytest
+
+from gene2vec_amd import _native as N
+from gene2vec_amd import engine as E
+from oracle import shuffle_oracle as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda:0")
+
+
+def _perm(src_d, n, first, count, seed):
+    import torch
+    dst = torch.empty(count, dtype=torch.int64, device="cuda:0")
+    E.permute_items8(0, src_d.data_ptr(), dst.data_ptr(), n, first, count, seed)
+    torch.cuda.synchronize()
+    return dst
+
+
+@pytest.mark.parametrize("n", [1, 2, 3, 17, 1000, 4097, 1_000_003])
+def test_matches_oracle(n):
+    rng = np.random.Generator(np.random.PCG64(n))
+    # items = int32 pairs viewed as 8-byte words
+    pairs = rng.integers(-1, 24447, size=(n, 2), dtype=np.int32)
+    items = pairs.view(np.int64).reshape(-1)
+    src = _dev(items)
+    for seed in (0, 20250114, 2 ** 64 - 1):
+        got = _perm(src, n, 0, n, seed).cpu().numpy()
+        assert np.array_equal(got, S.permute_items(items, seed)), (n, seed)
+    # ragged shard in the middle
+    lo, cnt = n // 3, max(0, n - n // 3 - n // 5)
+    got = _perm(src, n, lo, cnt, 7).cpu().numpy()
+    assert np.array_equal(got, S.permute_items(items, 7, lo, cnt))
+
+
+def test_full_size_bijection_and_shards():
+    import torch
+    n = 100_000_000  # C2: every pair lands exactly once
+    src = torch.arange(n, dtype=torch.int64, device="cuda:0")
+    full = _perm(src, n, 0, n, 99)
+    srt, _ = torch.sort(full)
+    assert torch.equal(srt, src)
+    # 8 data-parallel shards of the same permutation = the full order
+    bounds = np.linspace(0, n, 9).astype(np.int64)
+    for r in range(8):
+        part = _perm(src, n, int(bounds[r]), int(bounds[r + 1] - bounds[r]), 99)
+        assert torch.equal(part, full[bounds[r]:bounds[r + 1]])
+    # a known sample of positions against the restatement
+    idx = np.random.Generator(np.random.PCG64(1)).integers(0, n, 4096)
+    assert np.array_equal(full[torch.from_numpy(idx).cuda()].cpu().numpy(),
+                          S.perm_at(n, 99, idx.astype(np.uint64)))
+
+
+def test_argument_errors():
+    import torch
+    src = torch.zeros(10, dtype=torch.int64, device="cuda:0")
+    dst = torch.zeros(10, dtype=torch.int64, device="cuda:0")
+    with pytest.raises(N.G2VError):
+        E.permute_items8(0, src.data_ptr(), dst.data_ptr(), 10, 5, 6, 1)
+    with pytest.raises(N.G2VError):
+        E.permute_items8(0, 0, dst.data_ptr(), 10, 0, 10, 1)
+    E.permute_items8(0, 0, 0, 10, 10, 0, 1)  # empty shard: nothing to do
