@@ -102,6 +102,7 @@ SIGNATURES = {
     "g2v_read_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "g2v_cosine_pairs": (C.c_int, [C.c_int, _vp, _i64, _i32, _vp, _vp, _i64, _vp]),
     "g2v_permute_items8": (C.c_int, [C.c_int, _vp, _vp, _i64, _i64, _i64, C.c_uint64, _vp]),
+    "g2v_first_occurrence_perm8": (C.c_int, [C.c_int, _vp, _i64, C.c_uint64, _i32, _vp, _vp]),
     "g2v_seeded_vectors": (C.c_int, [_vp, _i64, _i32, _vp]),
     "g2v_format_rows": (C.c_int, [_vp, _i64, _i32, _vp, _i64, _vp, _vp, _i32, _vp, _i64,
                                   C.POINTER(_i64)]),

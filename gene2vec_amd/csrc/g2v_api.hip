@@ -1122,6 +1122,19 @@ int g2v_permute_items8(int device, const void* src, void* dst, int64_t n_items, 
   return G2V_OK;
 }
 
+int g2v_first_occurrence_perm8(int device, const void* items, int64_t n_items, uint64_t seed,
+                               int32_t n_ids, int64_t* first, void* stream) {
+  REQUIRE(n_items >= 0 && n_ids >= 0, G2V_EINVAL, "bad sizes");
+  REQUIRE(n_items < (1ll << 62), G2V_ERANGE, "%lld items: at most 2^62", (long long)n_items);
+  REQUIRE((n_items == 0 || items) && (n_ids == 0 || first), G2V_EINVAL, "null device pointer");
+  if (n_ids == 0) return G2V_OK;
+  HIPCHK(hipSetDevice(device));
+  const PermKey pk = perm_key((uint64_t)n_items, seed);
+  HIPCHK(launch_first_occ_perm8(static_cast<const uint64_t*>(items), pk, n_ids, first,
+                                static_cast<hipStream_t>(stream)));
+  return G2V_OK;
+}
+
 int g2v_sync(g2v_ctx* c) {
   int rc = set_dev(c);
   if (rc) return rc;

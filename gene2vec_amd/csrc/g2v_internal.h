@@ -192,6 +192,8 @@ __host__ __device__ inline uint64_t perm_at(const PermKey& pk, uint64_t i) {
 }
 hipError_t launch_permute8(const uint64_t* src, uint64_t* dst, const PermKey& pk, int64_t first,
                            int64_t count, hipStream_t st);
+hipError_t launch_first_occ_perm8(const uint64_t* src, const PermKey& pk, int32_t n_ids,
+                                  int64_t* first, hipStream_t st);
 hipError_t launch_vocab(const int64_t* counts, double* cpow, int32_t V, double power,
                         double sample, uint32_t* cum, uint32_t* sample_int, int32_t* bkt,
                         hipStream_t st);

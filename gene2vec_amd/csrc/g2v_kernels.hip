@@ -560,4 +560,39 @@ hipError_t launch_permute8(const uint64_t* src, uint64_t* dst, const PermKey& pk
   return hipGetLastError();
 }
 
+// First occurrence of every id in the PERMUTED token stream (position 2i /
+// 2i+1 for the two genes of the pair at permuted index i): the vocabulary
+// scan of [ext] scan_vocab after a device shuffle -- gensim breaks count ties
+// by first occurrence.  A small grid sweeps the order front to back, so the
+// frequent ids are set within the first sweep and later threads find a
+// smaller value and skip the atomic.
+__global__ void k_first_occ_perm8(const uint64_t* __restrict__ src, PermKey pk, int32_t n_ids,
+                                  unsigned long long* __restrict__ first) {
+  const int64_t n = (int64_t)pk.n;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t item = src[perm_at(pk, (uint64_t)i)];
+    const int32_t ab[2] = {(int32_t)(uint32_t)item, (int32_t)(uint32_t)(item >> 32)};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int32_t w = ab[k];
+      const unsigned long long pos = 2ull * (unsigned long long)i + (unsigned long long)k;
+      if (w >= 0 && w < n_ids && __hip_atomic_load(first + w, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) > pos)
+        atomicMin(first + w, pos);
+    }
+  }
+}
+
+// first[] starts all-ones: an id that never occurs reads -1 as int64
+hipError_t launch_first_occ_perm8(const uint64_t* src, const PermKey& pk, int32_t n_ids,
+                                  int64_t* first, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(first, 0xFF, sizeof(int64_t) * (size_t)n_ids, st);
+  if (e != hipSuccess || pk.n == 0) return e;
+  const int64_t blocks = std::min<int64_t>(((int64_t)pk.n + 255) / 256, 2048);
+  hipLaunchKernelGGL(k_first_occ_perm8, dim3((unsigned)blocks), dim3(256), 0, st, src, pk, n_ids,
+                     reinterpret_cast<unsigned long long*>(first));
+  return hipGetLastError();
+}
+
 }  // namespace g2v

@@ -81,6 +81,15 @@ def permute_items8(device, src_ptr, dst_ptr, n_items, first, count, seed, stream
                                        C.c_void_p(stream) if stream else None))
 
 
+def first_occurrence_perm8(device, items_ptr, n_items, seed, n_ids, first_ptr, stream=None):
+    """g2v_first_occurrence_perm8: int64 first[n_ids] (device) = each id's first
+    token position in the order permute_items8(seed) gives, -1 if absent."""
+    N.check(N.lib().g2v_first_occurrence_perm8(int(device), C.c_void_p(items_ptr), int(n_items),
+                                               int(seed) % 2 ** 64, int(n_ids),
+                                               C.c_void_p(first_ptr),
+                                               C.c_void_p(stream) if stream else None))
+
+
 def count_ids(ids, V):
     ids = np.ascontiguousarray(ids, dtype=np.int32)
     counts = np.zeros(V, dtype=np.int64)

@@ -94,14 +94,33 @@ def _sentences(corpus, pairs_only):
     return (None, 2) if pairs_only else (corpus.sent_off, 0)
 
 
+def _device_raw_counts(corpus, seed, device):
+    """{word: count} in first-occurrence order of the corpus as
+    g2v_permute_items8(seed) orders it ([ext] scan_vocab after the first
+    shuffle, src/gene2vec.py:52), scanned on the GPU without materialising
+    that order (g2v_first_occurrence_perm8)"""
+    import torch
+    dev = torch.device("cuda", device)
+    raw = torch.from_numpy(np.ascontiguousarray(corpus.tokens).view(np.int64)).to(dev)
+    first = torch.empty(len(corpus.words), dtype=torch.int64, device=dev)
+    st = torch.cuda.current_stream(dev)
+    E.first_occurrence_perm8(device, raw.data_ptr(), raw.numel(), seed, len(corpus.words),
+                             first.data_ptr(), st.cuda_stream)
+    f = first.cpu().numpy()
+    del raw
+    present = np.nonzero(f >= 0)[0]
+    fo = present[np.argsort(f[present], kind="stable")]
+    return {corpus.words[i]: int(corpus.counts[i]) for i in fo}
+
+
 class _DeviceOrder:
-    """``--shuffle device``: the pair corpus stays in HBM in the order of the
-    first shuffle (src/gene2vec.py:52, CPython-exact: it fixes the vocabulary
-    order); every later reshuffle (:80, an unseeded random.shuffle in the
-    reference, so any uniform permutation is as faithful) is a keyed
-    permutation of that order evaluated on the GPU, each data-parallel rank
-    gathering only its own shard (g2v_permute_items8).  Replaces a serial
-    host Fisher-Yates over the whole corpus on every rank and the per-iteration
+    """``--shuffle device``: the pair corpus stays in HBM in file order, and
+    every shuffle of the reference -- the first (src/gene2vec.py:52) and the
+    reshuffle before each later iteration (:80), unseeded random.shuffle
+    calls, so any uniform permutation is as faithful -- is a keyed permutation
+    of it evaluated on the GPU, each data-parallel rank gathering only its own
+    shard (g2v_permute_items8).  Replaces a serial host Fisher-Yates over the
+    whole corpus per iteration on every rank and the per-iteration
     host-to-device copy of the tokens."""
 
     def __init__(self, tok, ids, device, rank, world):
@@ -118,20 +137,16 @@ class _DeviceOrder:
         self.buf = None
 
     def shard(self, seed):
-        """(ptr, n_tokens, keepalive) of this rank's pairs; seed None = the
-        first-shuffle order itself (iteration 1)"""
+        """(ptr, n_tokens, keepalive) of this rank's pairs in the order of
+        permutation `seed`"""
         torch = self.torch
-        if seed is None:
-            t = self.base[self.s0:self.s1]
-        else:
-            if self.buf is None:
-                self.buf = torch.empty(self.s1 - self.s0, dtype=torch.int64, device=self.dev)
-            st = torch.cuda.current_stream(self.dev)
-            E.permute_items8(self.device, self.base.data_ptr(), self.buf.data_ptr(), self.n,
-                             self.s0, self.s1 - self.s0, seed, st.cuda_stream)
-            st.synchronize()  # the engine reads it on its own stream
-            t = self.buf
-        return t.data_ptr(), 2 * t.numel(), t
+        if self.buf is None:
+            self.buf = torch.empty(self.s1 - self.s0, dtype=torch.int64, device=self.dev)
+        st = torch.cuda.current_stream(self.dev)
+        E.permute_items8(self.device, self.base.data_ptr(), self.buf.data_ptr(), self.n, self.s0,
+                         self.s1 - self.s0, seed, st.cuda_stream)
+        st.synchronize()  # the engine reads it on its own stream
+        return self.buf.data_ptr(), 2 * self.buf.numel(), self.buf
 
 
 class _Exporter:
@@ -254,12 +269,13 @@ def main(argv=None):
             # the first one (src/gene2vec.py:52) from a newline count while the
             # files are tokenised
             n_lines = ingest.count_lines(paths)
-            n_shuffles = 1 if shuffle_mode == "device" else max(1, args.iters)
-            pipe = ingest.ShufflePipeline(n_lines, rng, n_shuffles)
+            if shuffle_mode == "python":
+                pipe = ingest.ShufflePipeline(n_lines, rng, max(1, args.iters))
             try:
                 corpus = ingest.read_corpus(paths)
             except BaseException:
-                pipe.close(wait=True)
+                if pipe is not None:
+                    pipe.close(wait=True)
                 raise
             n_pairs = corpus.n_sent
         else:
@@ -272,24 +288,27 @@ def main(argv=None):
         print("--shuffle device needs --native-ingest and a pairs-only corpus: "
               "using Python's shuffle")
         shuffle_mode = "python"
+        if corpus is not None:
+            pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
     dorder = None
+    perm_seed = None
     print(datetime.datetime.now())
     print("shuffle start " + str(n_pairs))
     exporter = _Exporter(not args.no_txt, not args.no_w2v, args.w2v_binary)
     with ph("shuffle"):
-        if corpus is not None:
+        if shuffle_mode == "device":
+            # the first shuffle (:52) is a device permutation too: one draw,
+            # the same on every rank; the vocabulary scan follows its order
+            perm_seed = rng.getrandbits(64)
+        elif corpus is not None:
             # this shuffle and the reshuffle before every later iteration (:80)
             # are drawn ahead on host threads while the GPU trains
             if corpus.n_sent != n_lines:  # cannot happen; never shuffle the wrong n
                 pipe.close(wait=True)
-                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, n_shuffles)
+                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
             perm = pipe.next()
             corpus.permute_(perm)
             pipe.release(perm)
-            if shuffle_mode == "python" and n_shuffles == 1 and args.iters > 1:
-                # fell back from --shuffle device: draw the later reshuffles too
-                pipe.close(wait=True)
-                pipe = ingest.ShufflePipeline(corpus.n_sent, rng, args.iters - 1)
         else:
             rng.shuffle(gene_pairs)
     print(datetime.datetime.now())
@@ -316,7 +335,11 @@ def main(argv=None):
                 else:
                     with ph("vocab"):
                         model = Word2Vec(**kw)
-                        model._build_from_counts(corpus.vocab_raw_counts())
+                        if shuffle_mode == "device":
+                            model._build_from_counts(
+                                _device_raw_counts(corpus, perm_seed, args.device))
+                        else:
+                            model._build_from_counts(corpus.vocab_raw_counts())
                         model.corpus_count = corpus.n_sent
                         model.corpus_total_words = int(len(corpus.tokens))
                         ids = _vocab_ids(model, corpus)
@@ -327,7 +350,8 @@ def main(argv=None):
                             dorder = _DeviceOrder(tok, _vocab_ids(model, corpus), args.device,
                                                   rank, world)
                             model.train_ids(None, None, 2, total_examples=model.corpus_count,
-                                            epochs=model.iter, device_tokens=dorder.shard(None))
+                                            epochs=model.iter,
+                                            device_tokens=dorder.shard(perm_seed))
                         else:
                             model.train_ids(tok, *_sentences(corpus, pairs_only),
                                             total_examples=model.corpus_count,

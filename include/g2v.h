@@ -316,6 +316,15 @@ int g2v_cosine_pairs(int device, const float *vectors, int64_t V, int32_t D, con
 int g2v_permute_items8(int device, const void *src, void *dst, int64_t n_items, int64_t first,
                        int64_t count, uint64_t seed, void *stream);
 
+/* The vocabulary scan ([ext] scan_vocab: gensim breaks count ties by first
+ * occurrence) of the order g2v_permute_items8 gives with the same seed,
+ * without materialising it: first[w] = the smallest token position (2i or
+ * 2i+1 for the pair at permuted index i) of id w, -1 when w never occurs;
+ * ids outside [0, n_ids) (OOV = -1) are skipped.  items: the n_items pairs as
+ * 8-byte items, first: int64[n_ids], both device memory; enqueued on stream. */
+int g2v_first_occurrence_perm8(int device, const void *items, int64_t n_items, uint64_t seed,
+                               int32_t n_ids, int64_t *first, void *stream);
+
 /* ---- host-native helpers (no device work) -------------------------------------- */
 /* [ext] Word2VecTrainables.seeded_vector for every row: row i =
  * (RandomState(seeds[i]).rand(D) - 0.5) / D as float32, seeds[i] =

@@ -71,3 +71,17 @@ def permute_items(src, seed, first=0, count=None):
     if count == 0:
         return src[:0].copy()
     return src[perm_at(n, seed, np.arange(first, first + count, dtype=np.uint64))]
+
+
+def first_occurrence(pairs, seed, n_ids):
+    """g2v_first_occurrence_perm8 restated: pairs int32[n][2]; first token
+    position of every id in [0, n_ids) in the permuted order, -1 if absent."""
+    n = len(pairs)
+    first = np.full(n_ids, -1, dtype=np.int64)
+    if n == 0:
+        return first
+    flat = np.asarray(pairs)[perm_at(n, seed, np.arange(n, dtype=np.uint64))].reshape(-1)
+    ok = (flat >= 0) & (flat < n_ids)
+    ids, pos = np.unique(flat[ok], return_index=True)
+    first[ids] = np.nonzero(ok)[0][pos]
+    return first

@@ -55,7 +55,9 @@ def test_cli_data_parallel_two_ranks(tmp_path):
     opts = ["--iters", "4", "--dim", "64", "--hash", "crc32", "--shuffle-seed", "5",
             "--native-ingest", "--no-txt", "--merge-every-jobs", "8"]
 
-    cli_main([str(data), str(tmp_path / "single"), "txt"] + opts)
+    # under torchrun the CLI shuffles on the device (--shuffle device); the
+    # single-process run takes the same shuffles, so both see one vocabulary
+    cli_main([str(data), str(tmp_path / "single"), "txt", "--shuffle", "device"] + opts)
 
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))

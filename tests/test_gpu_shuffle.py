@@ -70,3 +70,17 @@ def test_argument_errors():
     with pytest.raises(N.G2VError):
         E.permute_items8(0, 0, dst.data_ptr(), 10, 0, 10, 1)
     E.permute_items8(0, 0, 0, 10, 10, 0, 1)  # empty shard: nothing to do
+
+
+@pytest.mark.parametrize("n,n_ids", [(1, 3), (5000, 40), (200_003, 3000)])
+def test_first_occurrence_matches_oracle(n, n_ids):
+    import torch
+    rng = np.random.Generator(np.random.PCG64(n))
+    # Zipf-like ids with OOV (-1) and ids past n_ids (skipped)
+    pairs = (rng.zipf(1.3, size=(n, 2)) - 2).clip(-1, n_ids + 5).astype(np.int32)
+    src = _dev(pairs.view(np.int64).reshape(-1))
+    first = torch.empty(n_ids, dtype=torch.int64, device="cuda:0")
+    for seed in (3, 2 ** 63 + 11):
+        E.first_occurrence_perm8(0, src.data_ptr(), n, seed, n_ids, first.data_ptr())
+        torch.cuda.synchronize()
+        assert np.array_equal(first.cpu().numpy(), S.first_occurrence(pairs, seed, n_ids))
