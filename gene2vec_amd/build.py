@@ -86,3 +86,26 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 if __name__ == "__main__":
     print(build(force="--force" in sys.argv, verbose=True))
+
+
+EXAMPLES = os.path.join(os.path.dirname(HERE), "examples")
+
+
+def build_examples(verbose=False):
+    """examples/g2v_train: a Python-free host of the C ABI (gcc, links libg2v.so
+    through an rpath relative to the binary)."""
+    src = os.path.join(EXAMPLES, "g2v_train.c")
+    out = os.path.join(EXAMPLES, "g2v_train")
+    lib = os.path.join(HERE, "libg2v.so")
+    if (os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src)
+            and os.path.getmtime(out) >= os.path.getmtime(lib)):
+        return out
+    cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wextra",
+           "-I", os.path.join(os.path.dirname(HERE), "include"), src, "-L", HERE, "-lg2v",
+           "-Wl,-rpath,$ORIGIN/../gene2vec_amd", "-o", out]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"gcc failed on {src}:\n{r.stderr}")
+    return out
