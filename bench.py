@@ -78,6 +78,9 @@ def parse():
                    help="replica merge rule (gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
     p.add_argument("--stripe", default="", help="hot-row stripes ROWSxCOPIES (default: library's)")
+    p.add_argument("--sample-overlap", type=int, choices=(0, 1), default=None,
+                   help="G2V_OPT_SAMPLE_OVERLAP (sampler of segment s+1 under segment s's "
+                        "SGNS kernel; default: the library's)")
     p.add_argument("--seg-jobs", type=int, default=0,
                    help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
@@ -156,6 +159,8 @@ def main():
         eng.set_option(N.OPT_STRIPE_COPIES, sc)
     if a.seg_jobs:
         eng.set_option(N.OPT_SEG_JOBS, a.seg_jobs)
+    if a.sample_overlap is not None:
+        eng.set_option(N.OPT_SAMPLE_OVERLAP, a.sample_overlap)
     # a dedicated (non-default) stream: g2v kernels, RCCL all-reduces and the
     # timing events are all ordered on it
     stream = torch.cuda.Stream(dev)

@@ -39,6 +39,7 @@ OPT_DEBUG_WRITE = 6
 OPT_STRIPE_ROWS = 7
 OPT_STRIPE_COPIES = 8
 OPT_ATOMIC_OVERLAP = 9
+OPT_SAMPLE_OVERLAP = 10
 BATCH_WORDS = 10000
 MAX_DIM = 512
 TXT_MATRIX = 0

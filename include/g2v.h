@@ -123,7 +123,10 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_ATOMIC_OVERLAP Hogwild kernel: 1 = a wave's table atomics retire
  *                         behind its next example's compute, 0 = they land
  *                         before it (less staleness per wave, more waves
- *                         needed for the same rate) [1] */
+ *                         needed for the same rate) [1]
+ *   G2V_OPT_SAMPLE_OVERLAP 1 = sample segment s+1 on a side stream while
+ *                         segment s trains (double-buffered records; the
+ *                         segments still train in order) [1] */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
@@ -133,6 +136,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_STRIPE_ROWS 7
 #define G2V_OPT_STRIPE_COPIES 8
 #define G2V_OPT_ATOMIC_OVERLAP 9
+#define G2V_OPT_SAMPLE_OVERLAP 10
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest
