@@ -338,12 +338,15 @@ def main():
         sd = E.job_seeds(np.random.RandomState(1), len(jsc) - 1)
         ld_cpu = (D + 15) // 16 * 16  # rows on 64-B lines of their own (no false sharing)
 
-        def cpu_run(threads):
+        def cpu_run(threads, n=ns):
             c0 = syn0_h.copy()
             c1 = np.zeros_like(c0)
+            js_n = jsc if n == ns else E.plan_jobs(n_sent=n, sent_len=2)
+            al_n = al if n == ns else E.job_alphas(js_n, n).astype(np.float32)
             t = time.perf_counter()
-            CO.train(tok[:2 * ns], off, jsc, al, sd, si, a.sample != 0, cum, c0, c1,
-                     np.ones(V, np.float32), K, nthreads=threads, ld=ld_cpu)
+            CO.train(tok[:2 * n], off[:n + 1], js_n, al_n, sd[:len(js_n) - 1], si,
+                     a.sample != 0, cum, c0, c1, np.ones(V, np.float32), K, nthreads=threads,
+                     ld=ld_cpu)
             return time.perf_counter() - t
 
         dt = cpu_run(ncpu)
@@ -354,6 +357,14 @@ def main():
                          f"CPU this process may use (os.cpu_count() {host_cores}, affinity "
                          f"{affinity}, cgroup quota {quota}), rows padded to {ld_cpu} floats, "
                          f"{dt:.2f} s"}
+        if host_cores != ncpu:
+            # os.cpu_count() threads as well (SURVEY 8(d) "all host cores"), on a
+            # smaller sample: under a CPU quota they time-share `usable` CPUs
+            nh = min(ns, 10_000_000)
+            dh = cpu_run(host_cores, nh)
+            cpu["value_host_cores_threads"] = round(nh / dh, 1)
+            cpu["host_cores_sample"] = (f"first {nh} pairs, {host_cores} threads "
+                                        f"(os.cpu_count()), {dh:.2f} s")
         if a.cpu_extra:
             for th in sorted({1, host_cores} - {ncpu}):
                 d = cpu_run(th)

@@ -476,7 +476,14 @@ int g2v_destroy(g2v_ctx* c) {
 int g2v_set_stream(g2v_ctx* c, void* s) {
   int rc = set_dev(c);
   if (rc) return rc;
-  c->stream = s ? (hipStream_t)s : c->own_stream;
+  hipStream_t next = s ? (hipStream_t)s : c->own_stream;
+  if (next != c->stream) {
+    // the context's buffers are stream-ordered on one stream at a time: work
+    // queued on the previous stream (and the side stream) finishes first
+    if (c->stream) HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->side) HIPCHK(hipStreamSynchronize(c->side));
+  }
+  c->stream = next;
   return G2V_OK;
 }
 

@@ -98,7 +98,8 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
                int32_t window, g2v_ctx **out);
 int g2v_destroy(g2v_ctx *ctx);
 /* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+ * NULL restores the context's own stream.  Work already queued on the
+ * previous stream completes first (synchronises when the stream changes). */
 int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 /* Tuning knobs (defaults in brackets):
  *   G2V_OPT_HOT_ROWS      rows [0, n) -- the n most frequent genes -- are updated
