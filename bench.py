@@ -106,6 +106,11 @@ def parse():
 
 def main():
     a = parse()
+    # stdout carries exactly one JSON line: the libraries' own chatter (RCCL
+    # prints its version banner from C on fd 1) goes to stderr until then
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -401,7 +406,8 @@ def main():
             "step_ms_rank0": step_ms, "step_ms_median_rank0": float(np.median(step_ms)),
             "corpus_gen_s": round(t_corpus, 2),
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     eng.close()
     if use_dist:
         dist.destroy_process_group()

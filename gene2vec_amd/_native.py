@@ -40,6 +40,8 @@ OPT_STRIPE_ROWS = 7
 OPT_STRIPE_COPIES = 8
 OPT_ATOMIC_OVERLAP = 9
 OPT_SAMPLE_OVERLAP = 10
+OPT_MERGE_EVERY_JOBS = 11
+OPT_MERGE_RULE = 12
 BATCH_WORDS = 10000
 MAX_DIM = 512
 TXT_MATRIX = 0

@@ -108,6 +108,8 @@ struct g2v_ctx {
   int stripe_rows = 8, stripe_copies = 0;  // copies 0 = auto (stripe_copies_eff)
   int atomic_overlap = 1;
   int sample_overlap = 1;  // measured +1.2 % at C2
+  int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
+  int merge_rule = 0;
   float* stripe = nullptr;
   int64_t stripe_cap = 0;
   uint32_t* dbg16 = nullptr;  // ablation 3: packed-f16 atomic scratch [2][V + stripes][ld/2]
@@ -546,6 +548,15 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value == 0 || value == 1, G2V_EINVAL, "sample overlap must be 0 or 1");
       c->sample_overlap = (int)value;
       return G2V_OK;
+    case G2V_OPT_MERGE_EVERY_JOBS:
+      REQUIRE(value >= 0, G2V_EINVAL, "merge cadence must be >= 0");
+      c->merge_every = value;
+      return G2V_OK;
+    case G2V_OPT_MERGE_RULE:
+      REQUIRE(value == G2V_MERGE_TOUCH || value == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %lld",
+              (long long)value);
+      c->merge_rule = (int)value;
+      return G2V_OK;
     case G2V_OPT_GRID:
       REQUIRE(value >= 0, G2V_EINVAL, "grid must be >= 0");
       c->grid_user = value > 0;
@@ -568,6 +579,8 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_STRIPE_COPIES: *out = stripe_copies_eff(c); return G2V_OK;
     case G2V_OPT_ATOMIC_OVERLAP: *out = c->atomic_overlap; return G2V_OK;
     case G2V_OPT_SAMPLE_OVERLAP: *out = c->sample_overlap; return G2V_OK;
+    case G2V_OPT_MERGE_EVERY_JOBS: *out = c->merge_every; return G2V_OK;
+    case G2V_OPT_MERGE_RULE: *out = c->merge_rule; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -953,6 +966,8 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   return G2V_OK;
 }
 
+static int merge_now(g2v_ctx* c, int rule);
+
 extern "C" {
 
 int g2v_plan_jobs(const int64_t* sent_off, int64_t n_sent, int64_t sent_len, int64_t batch_words,
@@ -1024,13 +1039,31 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
   const bool timing = flags & G2V_FLAG_TIMING;
   const bool closs = flags & G2V_FLAG_COMPUTE_LOSS;
   if ((rc = upload_jobs(c, job_sent, job_alpha, job_seed, n_jobs))) return rc;
-  const int64_t n_seg = (n_jobs + c->seg_jobs - 1) / c->seg_jobs;
+  // segments of <= seg_jobs jobs; with G2V_OPT_MERGE_EVERY_JOBS and a
+  // communicator, windows of merge_every jobs end with a replica merge
+  // (g2v_average's kernels and all-reduce on the same stream), so a whole
+  // data-parallel epoch is one call and the sampler overlap spans the merges
+  struct Seg {
+    int64_t j0, nj;
+    bool merge;
+  };
+  std::vector<Seg> segs;
+  const bool merging = c->comm && c->merge_every > 0;
+  const int64_t win = merging ? c->merge_every : n_jobs;
+  for (int64_t w0 = 0; w0 < n_jobs; w0 += win) {
+    const int64_t w1 = std::min<int64_t>(n_jobs, w0 + win);
+    for (int64_t j0 = w0; j0 < w1; j0 += c->seg_jobs) {
+      const int64_t nj = std::min<int64_t>(c->seg_jobs, w1 - j0);
+      segs.push_back({j0, nj, merging && j0 + nj == w1});
+    }
+  }
+  const int64_t n_seg = (int64_t)segs.size();
   if (!c->sample_overlap || n_seg == 1) {
-    for (int64_t j0 = 0; j0 < n_jobs; j0 += c->seg_jobs) {
-      const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
-      if ((rc = sample_segment(c, j0, nj, timing))) return rc;
-      if ((rc = run_sgns(c, c->d_job_exoff + nj, mode, timing, closs, c->syn0, c->syn1)))
+    for (const Seg& g : segs) {
+      if ((rc = sample_segment(c, g.j0, g.nj, timing))) return rc;
+      if ((rc = run_sgns(c, c->d_job_exoff + g.nj, mode, timing, closs, c->syn0, c->syn1)))
         return rc;
+      if (g.merge && (rc = merge_now(c, c->merge_rule))) return rc;
     }
     c->jobs += n_jobs;
     return G2V_OK;
@@ -1046,26 +1079,24 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
   }
   HIPCHK(hipEventRecord(c->ev_up, c->stream));  // job tables uploaded, counters reset
   HIPCHK(hipStreamWaitEvent(c->side, c->ev_up, 0));
-  if ((rc = sample_segment(c, 0, std::min<int64_t>(c->seg_jobs, n_jobs), timing, 0, c->side)))
-    return rc;
+  if ((rc = sample_segment(c, segs[0].j0, segs[0].nj, timing, 0, c->side))) return rc;
   HIPCHK(hipEventRecord(c->ev_samp[0], c->side));
   for (int64_t sg = 0; sg < n_seg; ++sg) {
     const int b = (int)(sg & 1);
-    const int64_t j0 = sg * c->seg_jobs;
-    const int64_t nj = std::min<int64_t>(c->seg_jobs, n_jobs - j0);
+    const Seg& g = segs[(size_t)sg];
     if (sg + 1 < n_seg) {
-      const int64_t j1 = j0 + nj;
-      const int64_t nj1 = std::min<int64_t>(c->seg_jobs, n_jobs - j1);
+      const Seg& h = segs[(size_t)sg + 1];
       // workspace 1-b was last read by segment sg-1's SGNS kernel
       if (sg >= 1) HIPCHK(hipStreamWaitEvent(c->side, c->ev_sgns[1 - b], 0));
-      if ((rc = sample_segment(c, j1, nj1, timing, 1 - b, c->side))) return rc;
+      if ((rc = sample_segment(c, h.j0, h.nj, timing, 1 - b, c->side))) return rc;
       HIPCHK(hipEventRecord(c->ev_samp[1 - b], c->side));
     }
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_samp[b], 0));
-    if ((rc = run_sgns(c, (b ? c->d_job_exoff2 : c->d_job_exoff) + nj, mode, timing, closs,
+    if ((rc = run_sgns(c, (b ? c->d_job_exoff2 : c->d_job_exoff) + g.nj, mode, timing, closs,
                        c->syn0, c->syn1, b ? c->d_rec2 : c->d_rec)))
       return rc;
     HIPCHK(hipEventRecord(c->ev_sgns[b], c->stream));
+    if (g.merge && (rc = merge_now(c, c->merge_rule))) return rc;
   }
   c->jobs += n_jobs;
   return G2V_OK;
@@ -1337,7 +1368,16 @@ int g2v_average(g2v_ctx* c, int rule) {
   int rc = set_dev(c);
   if (rc) return rc;
   REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %d", rule);
-  if (!c->comm) return G2V_OK;  // one rank: the full path runs (an identity on the values)
+  if (!c->comm) return G2V_OK;  // no communicator: nothing to merge with
+  return merge_now(c, rule);
+}
+
+}  // extern "C"
+
+// the merge of g2v_average on the context's stream (also run inside g2v_train
+// at G2V_OPT_MERGE_EVERY_JOBS window ends); a one-rank communicator runs the
+// full path, an identity on the values
+static int merge_now(g2v_ctx* c, int rule) {
   REQUIRE(c->merge_valid && c->merge_ld == c->ld, G2V_ESTATE,
           "no merge snapshot (g2v_comm_init / g2v_merge_snapshot)");
   const Rccl& r = rccl();
@@ -1362,6 +1402,8 @@ int g2v_average(g2v_ctx* c, int rule) {
                               rule, 1.0f / (float)c->nranks, c->stream));
   return G2V_OK;
 }
+
+extern "C" {
 
 int g2v_average_local(g2v_ctx* const* ctxs, int n, int rule) {
   REQUIRE(ctxs != nullptr && n >= 1 && n <= kMaxLocalReplicas, G2V_EINVAL,

@@ -186,6 +186,26 @@ class ReplicaTrainer:
         kw = {"timing": timing}
         if compute_loss:
             kw["compute_loss"] = True
+        if self.backend == "rccl" and world > 1:
+            # one g2v_train call for the whole epoch: libg2v merges at the end
+            # of every window of `every` jobs on its own stream
+            # (G2V_OPT_MERGE_EVERY_JOBS), so the sampler of the next segment
+            # keeps running under the update kernel across merges; a rank with
+            # fewer windows joins the remaining merges afterwards
+            from . import _native as N
+            own = (n_jobs + every - 1) // every
+            self.engine.set_option(N.OPT_MERGE_RULE, MERGE_RULES[self.merge])
+            self.engine.set_option(N.OPT_MERGE_EVERY_JOBS, every)
+            try:
+                if n_jobs > 0:
+                    self.engine.train(job_sent, alphas, seeds, self.mode, **kw)
+            finally:
+                # later train() calls of this engine (not data-parallel) merge nothing
+                self.engine.set_option(N.OPT_MERGE_EVERY_JOBS, 0)
+            for _ in range(n_win - own):
+                self.engine.average(MERGE_RULES[self.merge])
+            self.averages += n_win
+            return
         for w in range(n_win):
             j0 = w * every
             j1 = min(n_jobs, j0 + every)

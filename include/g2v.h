@@ -127,7 +127,13 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         needed for the same rate) [1]
  *   G2V_OPT_SAMPLE_OVERLAP 1 = sample segment s+1 on a side stream while
  *                         segment s trains (double-buffered records; the
- *                         segments still train in order) [1] */
+ *                         segments still train in order) [1]
+ *   G2V_OPT_MERGE_EVERY_JOBS with a communicator (g2v_comm_init): g2v_train
+ *                         ends every window of this many jobs -- and the
+ *                         call's last, shorter one -- with the replica merge
+ *                         of g2v_average, on the same stream; every rank must
+ *                         make the same number of merges (0 = off) [0]
+ *   G2V_OPT_MERGE_RULE    rule of those merges, G2V_MERGE_TOUCH / _MEAN [TOUCH] */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
@@ -138,6 +144,8 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_STRIPE_COPIES 8
 #define G2V_OPT_ATOMIC_OVERLAP 9
 #define G2V_OPT_SAMPLE_OVERLAP 10
+#define G2V_OPT_MERGE_EVERY_JOBS 11
+#define G2V_OPT_MERGE_RULE 12
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest

@@ -128,3 +128,37 @@ def test_rccl_one_rank_merge(rule):
     h0, h1 = e.get_weights()
     assert np.array_equal(h0, g0) and np.array_equal(h1, g1)
     e.close()
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_rccl_in_call_merges_equal_external(overlap):
+    """G2V_OPT_MERGE_EVERY_JOBS: one g2v_train call that merges at the end of
+    every window of 3 jobs (and of the shorter last window) trains and merges
+    exactly what separate per-window train calls with g2v_average in between
+    do -- SEQUENTIAL mode, one-rank communicator, so the results are bit for
+    bit; with and without the overlapped sampler."""
+    res = []
+    for inner in (False, True):
+        engs, syn0, syn1, n = _setup(1, n_pairs=36_000)
+        e = engs[0]
+        e.set_option(N.OPT_SEG_JOBS, 2)
+        e.set_option(N.OPT_SAMPLE_OVERLAP, overlap)
+        e.comm_init(E.SGNSEngine.comm_unique_id(), 1, 0)
+        js = E.plan_jobs(n_sent=n, sent_len=2)
+        al = E.job_alphas(js, n)
+        sd = E.job_seeds(np.random.RandomState(3), len(js) - 1)
+        nj = len(js) - 1
+        assert nj % 3 != 0  # a shorter last window
+        if inner:
+            e.set_option(N.OPT_MERGE_RULE, N.MERGE_TOUCH)
+            e.set_option(N.OPT_MERGE_EVERY_JOBS, 3)
+            e.train(js, al, sd, N.MODE_SEQUENTIAL)
+            e.set_option(N.OPT_MERGE_EVERY_JOBS, 0)
+        else:
+            for j0 in range(0, nj, 3):
+                j1 = min(nj, j0 + 3)
+                e.train(js[j0:j1 + 1], al[j0:j1], sd[j0:j1], N.MODE_SEQUENTIAL)
+                e.average(N.MERGE_TOUCH)
+        res.append(e.get_weights())
+        e.close()
+    assert np.array_equal(res[0][0], res[1][0]) and np.array_equal(res[0][1], res[1][1])
