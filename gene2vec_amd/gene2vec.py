@@ -235,10 +235,11 @@ def main(argv=None):
     parser.add_argument("--merge-every-jobs", type=int, default=1024,
                         help="data-parallel replica merge cadence (gensim jobs per rank)")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
-                        help="reshuffles before iterations >= 2 (src/gene2vec.py:80): 'python' = "
-                             "CPython's random.shuffle bit for bit on the host; 'device' = a "
-                             "keyed permutation of the HBM-resident pairs on the GPU (needs "
-                             "--native-ingest and a pairs-only corpus; default under torchrun)")
+                        help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
+                             "random.shuffle bit for bit on the host; 'device' = keyed "
+                             "permutations of the HBM-resident pairs on the GPU, vocabulary "
+                             "scanned in the first one's order (needs --native-ingest and a "
+                             "pairs-only corpus; default under torchrun)")
     args = parser.parse_args(argv)
     rank, world = _init_dp(args)
     # data-parallel ranks would each redo a serial Fisher-Yates over the whole
