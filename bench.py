@@ -78,6 +78,8 @@ def parse():
                    help="replica merge rule (gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
     p.add_argument("--stripe", default="", help="hot-row stripes ROWSxCOPIES (default: library's)")
+    p.add_argument("--stripe2", default="",
+                   help="second stripe tier ENDROWxCOPIES, 0x4 = off (default: library's)")
     p.add_argument("--sample-overlap", type=int, choices=(0, 1), default=None,
                    help="G2V_OPT_SAMPLE_OVERLAP (sampler of segment s+1 under segment s's "
                         "SGNS kernel; default: the library's)")
@@ -162,6 +164,10 @@ def main():
         sr, sc = (int(x) for x in a.stripe.lower().split("x"))
         eng.set_option(N.OPT_STRIPE_ROWS, sr)
         eng.set_option(N.OPT_STRIPE_COPIES, sc)
+    if a.stripe2:
+        r2, c2 = (int(x) for x in a.stripe2.lower().split("x"))
+        eng.set_option(N.OPT_STRIPE2_ROWS, r2)
+        eng.set_option(N.OPT_STRIPE2_COPIES, c2)
     if a.seg_jobs:
         eng.set_option(N.OPT_SEG_JOBS, a.seg_jobs)
     if a.sample_overlap is not None:
@@ -292,7 +298,9 @@ def main():
                 "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
                 "atomic_frac": round(atomic_gbps / 1300.0, 4), "traffic_source": traffic_src,
                 "grid_workgroups": eng.get_option(N.OPT_GRID),
-                "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}"}
+                "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}",
+                "stripes_tier2": f"rows < {eng.get_option(N.OPT_STRIPE2_ROWS)} "
+                                 f"x{eng.get_option(N.OPT_STRIPE2_COPIES)}"}
 
     # ---- measured gather roof: the same kernel on the same index
     # stream with its table writes compiled out (G2V_OPT_DEBUG_WRITE=2) and a

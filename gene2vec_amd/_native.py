@@ -42,6 +42,8 @@ OPT_ATOMIC_OVERLAP = 9
 OPT_SAMPLE_OVERLAP = 10
 OPT_MERGE_EVERY_JOBS = 11
 OPT_MERGE_RULE = 12
+OPT_STRIPE2_ROWS = 13
+OPT_STRIPE2_COPIES = 14
 BATCH_WORDS = 10000
 MAX_DIM = 512
 TXT_MATRIX = 0

@@ -106,6 +106,9 @@ struct g2v_ctx {
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
   int stripe_rows = 8, stripe_copies = 0;  // copies 0 = auto (stripe_copies_eff)
+  int stripe2_rows = -1, stripe2_copies = 4;  // second tier: rows [stripe_rows, stripe2_rows), -1 = auto
+  float* stripe2 = nullptr;
+  int64_t stripe2_cap = 0;
   int atomic_overlap = 1;
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
@@ -214,6 +217,16 @@ constexpr double kStaleBudget = 125.0;
 static int stripe_copies_eff(const g2v_ctx* c) {
   if (c->stripe_copies > 0) return c->stripe_copies;
   return c->sgns_grid >= c->cus ? 16 : 8;
+}
+
+// Second stripe tier when G2V_OPT_STRIPE2_ROWS is not set: rows 8..19 get 4
+// copies each when the grid fills every CU (C2, interleaved A/B: 203.6 vs
+// 200.3 M ex/s; 24 rows 203.0, 32 rows 202.0), none below, where per-example
+// latency binds and the extra copy reads cost (C2 sample 0 at 162 WGs: 153.5
+// vs 157.0; C4 at 121: 36.6 vs 36.7)
+static int stripe2_rows_eff(const g2v_ctx* c) {
+  if (c->stripe2_rows >= 0) return c->stripe2_rows;
+  return c->sgns_grid >= c->cus ? 20 : 0;
 }
 
 static int default_grid(int cus, int K, int nv, double u_max) {
@@ -466,6 +479,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->merge_cnt);
   comm_destroy(c);
   dev_free(c->stripe);
+  dev_free(c->stripe2);
   dev_free(c->dbg16);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
@@ -532,6 +546,16 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value >= 0 && value <= 65536, G2V_EINVAL, "stripe rows out of [0, 65536]");
       c->stripe_rows = (int)value;
       return G2V_OK;
+    case G2V_OPT_STRIPE2_ROWS:
+      REQUIRE(value >= -1 && value <= (1 << 20), G2V_EINVAL,
+              "second-tier stripe rows out of range");
+      c->stripe2_rows = (int)value;  // -1: auto (stripe2_rows_eff)
+      return G2V_OK;
+    case G2V_OPT_STRIPE2_COPIES:
+      REQUIRE(value == 2 || value == 4 || value == 8, G2V_EINVAL,
+              "second-tier stripe copies must be 2, 4 or 8");
+      c->stripe2_copies = (int)value;
+      return G2V_OK;
     case G2V_OPT_STRIPE_COPIES:
       REQUIRE(value >= 0 && value <= 16, G2V_EINVAL, "stripe copies out of [0, 16]");
       c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
@@ -577,6 +601,8 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_DEBUG_WRITE: *out = c->debug_write; return G2V_OK;
     case G2V_OPT_STRIPE_ROWS: *out = c->stripe_rows; return G2V_OK;
     case G2V_OPT_STRIPE_COPIES: *out = stripe_copies_eff(c); return G2V_OK;
+    case G2V_OPT_STRIPE2_ROWS: *out = stripe2_rows_eff(c); return G2V_OK;
+    case G2V_OPT_STRIPE2_COPIES: *out = c->stripe2_copies; return G2V_OK;
     case G2V_OPT_ATOMIC_OVERLAP: *out = c->atomic_overlap; return G2V_OK;
     case G2V_OPT_SAMPLE_OVERLAP: *out = c->sample_overlap; return G2V_OK;
     case G2V_OPT_MERGE_EVERY_JOBS: *out = c->merge_every; return G2V_OK;
@@ -942,6 +968,21 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     }
   }
   s.stripe = c->stripe;
+  // second tier (not in the ablation builds, which address only the first)
+  const int64_t max_rows2 = kStripeMaxBytes / (2 * 4 * (int64_t)(c->stripe2_copies - 1) * c->ld);
+  const int r2 = (int)std::min<int64_t>(std::min(stripe2_rows_eff(c), c->V),
+                                        (int64_t)s.stripe_rows + max_rows2);
+  const bool tier2 = striped && c->debug_write == 0 && r2 > s.stripe_rows;
+  s.stripe2_rows = tier2 ? r2 : s.stripe_rows;
+  s.stripe2_copies = tier2 ? c->stripe2_copies : 1;
+  if (tier2) {
+    const int64_t need = 2 * (int64_t)(c->stripe2_copies - 1) * (r2 - s.stripe_rows) * c->ld;
+    if (need > c->stripe2_cap) {
+      if ((rc = dev_reserve(c->stream, &c->stripe2, &c->stripe2_cap, need))) return rc;
+      HIPCHK(hipMemsetAsync(c->stripe2, 0, sizeof(float) * c->stripe2_cap, c->stream));
+    }
+  }
+  s.stripe2 = c->stripe2;
   if (c->debug_write == 3 || c->debug_write == 4) {
     const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
     const int64_t words = rows * c->ld * (c->debug_write == 4 ? 2 : 1);
@@ -958,6 +999,11 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
   HIPCHK(launch_fold_stripes(c->syn0, c->syn1, c->stripe, s.stripe_rows, s.stripe_copies, c->ld,
                              c->nvec, c->stream));
+  if (tier2)
+    HIPCHK(launch_fold_stripes(c->syn0 + (int64_t)s.stripe_rows * c->ld,
+                               c->syn1 + (int64_t)s.stripe_rows * c->ld, c->stripe2,
+                               s.stripe2_rows - s.stripe_rows, s.stripe2_copies, c->ld, c->nvec,
+                               c->stream));
   if (timing) {
     HIPCHK(hipEventRecord(e1, c->stream));
     c->t_sgns.emplace_back(e0, e1);

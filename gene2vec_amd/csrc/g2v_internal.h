@@ -98,6 +98,11 @@ struct SgnsArgs {
   float* stripe;            // [2][stripe_copies-1][stripe_rows][ld]
   int stripe_rows;
   int stripe_copies;        // 1 = off
+  // second tier: rows [stripe_rows, stripe2_rows) with stripe2_copies-1 extra
+  // copies each (a power of two), layout [table][row - stripe_rows][copy][ld]
+  float* stripe2;
+  int stripe2_rows;         // <= stripe_rows = off
+  int stripe2_copies;
   int overlap;              // G2V_OPT_ATOMIC_OVERLAP
   unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]

@@ -57,18 +57,18 @@ __device__ __forceinline__ void load_main(float4 (&o)[NV], __amdgpu_buffer_rsrc_
 // past stripe_copies read an out-of-range offset (zeros, no memory access).
 constexpr int kStripeBatch = 7;
 constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
+// t: the row's index within its tier, rows / C: the tier's row count and copies
 template <int NV>
-__device__ __forceinline__ void add_stripes(float4 (&o)[NV], const SgnsArgs& a,
-                                            __amdgpu_buffer_rsrc_t rs, int t, int tbl, int rowb,
+__device__ __forceinline__ void add_stripes(float4 (&o)[NV], __amdgpu_buffer_rsrc_t rs, int t,
+                                            int tbl, int rows, int C, int rowb,
                                             const uint32_t (&loff)[NV]) {
-  const int C = a.stripe_copies;
   for (int c0 = 1; c0 < C; c0 += kStripeBatch) {
     float4 q[kStripeBatch][NV];
 #pragma unroll
     for (int j = 0; j < kStripeBatch; ++j) {
       const int c = c0 + j;
       const uint32_t base =
-          c < C ? (uint32_t)((int)stripe_row(tbl, t, c, a.stripe_rows, C) * rowb)
+          c < C ? (uint32_t)((int)stripe_row(tbl, t, c, rows, C) * rowb)
                 : (uint32_t)kStripeOob;
 #pragma unroll
       for (int v = 0; v < NV; ++v) q[j][v] = bload4<0>(rs, (int)(base + loff[v]));
@@ -86,13 +86,32 @@ __device__ __forceinline__ void add_stripes(float4 (&o)[NV], const SgnsArgs& a,
   }
 }
 
-// destination of an atomic delta for row t of table tbl: main or stripe copy c
-// (WR 4, ablation: the same rows of a scratch table the kernel never reads)
-// Byte offsets in 32 bits: g2v_create caps a table below 2 GiB (the buffer
-// offset range) and the stripe buffer below 1 GiB, so a row's offset is one
-// scalar multiply.
+// (c mod C) for 0 <= c < C + 32: the stripe copy of a row update without an
+// integer division per row
+__device__ __forceinline__ int wrap_copy(int c, int C) {
+  if (C == 1) return 0;
+  while (c >= C) c -= C;
+  return c;
+}
+
+// destination of an atomic delta for row t of table tbl: the main row or the
+// stripe copy (craw mod copies) of its tier (WR 4, ablation: the same rows of
+// a scratch table the kernel never reads).  Byte offsets in 32 bits:
+// g2v_create caps a table below 2 GiB (the buffer offset range) and the
+// stripe buffers below 1 GiB, so a row's offset is one scalar multiply.
 template <int WR = 0>
-__device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int c, int rowb) {
+__device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int craw, int rowb) {
+  if (t >= a.stripe_rows && t < a.stripe2_rows && WR != 4) {
+    const int c2 = craw & (a.stripe2_copies - 1);
+    if (c2 == 0)
+      return reinterpret_cast<float*>(reinterpret_cast<char*>(tbl ? a.wr1 : a.wr0) +
+                                      (uint32_t)(t * rowb));
+    const int sr =
+        (int)stripe_row(tbl, t - a.stripe_rows, c2, a.stripe2_rows - a.stripe_rows,
+                        a.stripe2_copies);
+    return reinterpret_cast<float*>(reinterpret_cast<char*>(a.stripe2) + (uint32_t)(sr * rowb));
+  }
+  const int c = wrap_copy(craw, a.stripe_copies);
   if (WR == 4) {
     const int64_t nrow = (int64_t)a.V + (int64_t)(a.stripe_copies - 1) * a.stripe_rows;
     const int64_t rr =
@@ -113,7 +132,8 @@ template <int K, int NV>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
                                              const int32_t* r, __amdgpu_buffer_rsrc_t r0,
                                              __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
-                                             int rowb, const uint32_t (&loff)[NV]) {
+                                             __amdgpu_buffer_rsrc_t rs2, int rowb,
+                                             const uint32_t (&loff)[NV]) {
   x.tg[0] = __builtin_amdgcn_readfirstlane(r[0]);
   x.input = __builtin_amdgcn_readfirstlane(r[1]);
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
@@ -129,11 +149,19 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
       for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  if (x.input < a.stripe_rows) add_stripes<NV>(x.l1, a, rs, x.input, 0, rowb, loff);
+  const int R1 = a.stripe_rows, R2 = a.stripe2_rows;
+  if (x.input < R1)
+    add_stripes<NV>(x.l1, rs, x.input, 0, R1, a.stripe_copies, rowb, loff);
+  else if (x.input < R2)
+    add_stripes<NV>(x.l1, rs2, x.input - R1, 0, R2 - R1, a.stripe2_copies, rowb, loff);
 #pragma unroll
-  for (int d = 0; d <= K; ++d)
-    if (x.tg[d] >= 0 && x.tg[d] < a.stripe_rows)
-      add_stripes<NV>(x.rw[d], a, rs, x.tg[d], 1, rowb, loff);
+  for (int d = 0; d <= K; ++d) {
+    if (x.tg[d] < 0) continue;
+    if (x.tg[d] < R1)
+      add_stripes<NV>(x.rw[d], rs, x.tg[d], 1, R1, a.stripe_copies, rowb, loff);
+    else if (x.tg[d] < R2)
+      add_stripes<NV>(x.rw[d], rs2, x.tg[d] - R1, 1, R2 - R1, a.stripe2_copies, rowb, loff);
+  }
 }
 
 // WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
@@ -188,14 +216,6 @@ __device__ __forceinline__ float uniform_f(float x) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
 
-// (c mod C) for 0 <= c < C + 32: the stripe copy of a row update without an
-// integer division per row
-__device__ __forceinline__ int wrap_copy(int c, int C) {
-  if (C == 1) return 0;
-  while (c >= C) c -= C;
-  return c;
-}
-
 __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
   unsigned int v = 0;
   if (lane == 0) v = atomicAdd(q, 1u);
@@ -228,6 +248,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   const __amdgpu_buffer_rsrc_t r1 = make_rsrc(a.rd1, tbytes);
   const __amdgpu_buffer_rsrc_t rs =
       make_rsrc(a.stripe, 2 * (int64_t)(a.stripe_copies - 1) * a.stripe_rows * a.ld * 4);
+  const __amdgpu_buffer_rsrc_t rs2 =
+      make_rsrc(a.stripe2, a.stripe2_rows > a.stripe_rows
+                               ? 2 * (int64_t)(a.stripe2_copies - 1) *
+                                     (a.stripe2_rows - a.stripe_rows) * a.ld * 4
+                               : 0);
   const int rowb = (int)a.ld * 4;
   float* s1 = s_l1[wid];
   float* sw = s_wk[wid];
@@ -256,7 +281,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
     int cbase = (int)(e_beg % (int64_t)a.stripe_copies);
     float lsum = 0.f;
     ExRegs<K, NV> x;
-    load_example<K, NV>(x, a, sr, r0, r1, rs, rowb, loff);
+    load_example<K, NV>(x, a, sr, r0, r1, rs, rs2, rowb, loff);
     // drain here, so the loop head only waits on the back edge's count
     // (vmcnt(#atomics of the previous example)); without it the two incoming
     // paths merge to vmcnt(0), which also waits for the previous atomics
@@ -370,7 +395,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       // before this pipelining: the Hogwild staleness stays what the grid
       // budget was measured with)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-      if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rowb, loff);
+      if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff);
 
       // ---- atomics of example e -----------------------------------------------
       if (WR == 3) {
@@ -404,9 +429,9 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work
 #pragma unroll
       for (int d = 0; d < NT; ++d)
-        emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, wrap_copy(cbase + d, a.stripe_copies), rowb),
+        emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb),
                          live[d], D, v1, g[d], lane);
-      emit_row<NV, WR>(upd_row<WR>(a, 0, input, wrap_copy(cbase + NT, a.stripe_copies), rowb),
+      emit_row<NV, WR>(upd_row<WR>(a, 0, input, cbase + NT, rowb),
                        any && WR != 5, D, vw, lf, lane);
       __builtin_amdgcn_wave_barrier();
       cbase = cbase + 1 == a.stripe_copies ? 0 : cbase + 1;

@@ -117,6 +117,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         atomics into a scratch table, 5 syn1neg atomics only
  *                         (syn0 never written) [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
+ *   G2V_OPT_STRIPE2_ROWS  second stripe tier: rows [STRIPE_ROWS, this) get
+ *                         STRIPE2_COPIES copies each (<= STRIPE_ROWS = off);
+ *                         -1 = auto: 20 when the SGNS grid fills every CU,
+ *                         else off [-1]
+ *   G2V_OPT_STRIPE2_COPIES copies per second-tier row: 2, 4 or 8 [4]
  *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off, 0 = auto: 16 when the
  *                         SGNS grid fills every CU, 8 below [0] (values stay
  *                         exact: readers sum the copies, each launch folds them
@@ -146,6 +151,8 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_SAMPLE_OVERLAP 10
 #define G2V_OPT_MERGE_EVERY_JOBS 11
 #define G2V_OPT_MERGE_RULE 12
+#define G2V_OPT_STRIPE2_ROWS 13
+#define G2V_OPT_STRIPE2_COPIES 14
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest

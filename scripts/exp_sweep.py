@@ -77,6 +77,10 @@ def main():
             r, c = cfg["stripe"].split("x")
             eng.set_option(N.OPT_STRIPE_ROWS, int(r))
             eng.set_option(N.OPT_STRIPE_COPIES, int(c))
+        if "stripe2" in cfg:  # second tier: END_ROWxCOPIES
+            r, c = cfg["stripe2"].split("x")
+            eng.set_option(N.OPT_STRIPE2_ROWS, int(r))
+            eng.set_option(N.OPT_STRIPE2_COPIES, int(c))
         if "seg" in cfg:
             eng.set_option(N.OPT_SEG_JOBS, int(cfg["seg"]))
         if "dbg" in cfg:

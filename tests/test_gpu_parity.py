@@ -426,10 +426,14 @@ def test_striping_keeps_values_exact():
     perm = rng.permutation(V).astype(np.int32).reshape(B, K + 2)
     center, inp, negs = perm[:, 0], perm[:, 1], perm[:, 2:]
     outs = []
-    for rows, copies in ((0, 1), (V, 8), (16, 3)):
+    # (rows, copies, second-tier end row, second-tier copies)
+    for rows, copies, r2, c2 in ((0, 1, 0, 4), (V, 8, 0, 4), (16, 3, 0, 4), (16, 3, 200, 4),
+                                 (8, 16, V, 2)):
         eng = E.SGNSEngine(V, D, K)
         eng.set_option(N.OPT_STRIPE_ROWS, rows)
         eng.set_option(N.OPT_STRIPE_COPIES, copies)
+        eng.set_option(N.OPT_STRIPE2_ROWS, r2)
+        eng.set_option(N.OPT_STRIPE2_COPIES, c2)
         eng.set_weights(syn0, syn1)
         eng.step_explicit(center, inp, negs, 0.025, N.MODE_HOGWILD)
         outs.append(eng.get_weights())
@@ -444,8 +448,8 @@ def test_striping_keeps_values_exact():
 def test_striped_reads_sum_every_copy():
     """One chunk (32 examples, one wave, deterministic) over 12 rows, so rows
     are re-read after their own earlier updates landed in stripe copies: 16
-    copies (two load batches of 7 + one), 3 copies and no striping agree to
-    float rounding of the copy sums."""
+    copies (two load batches of 7 + one), 3 copies, two-tier layouts and no
+    striping agree to float rounding of the copy sums."""
     D, K, B, V = 200, 5, 32, 12
     rng = np.random.Generator(np.random.PCG64(21))
     syn0 = ((rng.random((V, D)) - 0.5) / D * 40).astype(np.float32)
@@ -454,10 +458,14 @@ def test_striped_reads_sum_every_copy():
     inp = ((center + 1 + rng.integers(0, V - 1, B)) % V).astype(np.int32)
     negs = rng.integers(0, V, (B, K)).astype(np.int32)
     outs = []
-    for rows, copies in ((0, 1), (V, 16), (V, 3)):
+    # the last two: a second tier (rows 4..11 with 4 copies, rows 2..7 with 8)
+    for rows, copies, r2, c2 in ((0, 1, 0, 4), (V, 16, 0, 4), (V, 3, 0, 4), (4, 16, V, 4),
+                                 (2, 3, 8, 8)):
         eng = E.SGNSEngine(V, D, K)
         eng.set_option(N.OPT_STRIPE_ROWS, rows)
         eng.set_option(N.OPT_STRIPE_COPIES, copies)
+        eng.set_option(N.OPT_STRIPE2_ROWS, r2)
+        eng.set_option(N.OPT_STRIPE2_COPIES, c2)
         eng.set_weights(syn0, syn1)
         eng.step_explicit(center, inp, negs, 0.025, N.MODE_HOGWILD)
         outs.append(eng.get_weights())
