@@ -140,6 +140,60 @@ def allreduce_sum_float(v, group=None):
     return float(t.item())
 
 
+def gather_corpus(paths, group=None):
+    """Data-parallel native ingest (src/gene2vec.py:36-47): rank r tokenises
+    only the contiguous file range shard_range(len(paths), r, N), then the
+    ranks exchange their word lists (small) and token arrays (a collective
+    over the process group: RCCL over xGMI for nccl) and every rank assembles
+    the same corpus the single-process reader builds from all files in
+    order: words in first-occurrence order, counts summed, tokens
+    concatenated in file order.  Pair files only (the generator's output);
+    returns None when any rank's part is not all pairs, and the caller reads
+    every file itself."""
+    import torch
+    import torch.distributed as dist
+
+    from . import ingest
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    lo, hi = shard_range(len(paths), rank, world)
+    if hi > lo:
+        c = ingest.read_corpus(paths[lo:hi])
+        tok, words, counts, pairs = c.tokens, list(c.words), np.asarray(c.counts), c.pairs_only
+    else:  # more ranks than files
+        tok, words, counts, pairs = np.zeros(0, np.int32), [], np.zeros(0, np.int64), True
+    info = [None] * world
+    dist.all_gather_object(info, (words, counts, int(len(tok)), bool(pairs)), group=group)
+    if not all(i[3] for i in info):
+        return None
+    # global first-occurrence order: rank r's files follow rank r-1's
+    gidx, gwords, gcounts, remap = {}, [], [], None
+    for r, (w_r, c_r, _, _) in enumerate(info):
+        rm = np.empty(len(w_r), dtype=np.int32)
+        for i, w in enumerate(w_r):
+            j = gidx.get(w)
+            if j is None:
+                j = gidx[w] = len(gwords)
+                gwords.append(w)
+                gcounts.append(0)
+            gcounts[j] += int(c_r[i])
+            rm[i] = j
+        if r == rank:
+            remap = rm
+    mine = remap[tok] if len(tok) else tok
+    # tokens of every rank, padded to one length for the collective
+    sizes = [i[2] for i in info]
+    width = max(1, max(sizes))
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+    part = torch.zeros(width, dtype=torch.int32, device=dev)
+    part[:len(mine)] = torch.from_numpy(np.ascontiguousarray(mine, dtype=np.int32)).to(dev)
+    parts = [torch.empty(width, dtype=torch.int32, device=dev) for _ in range(world)]
+    dist.all_gather(parts, part, group=group)
+    full = np.concatenate([p[:n].cpu().numpy() for p, n in zip(parts, sizes)])
+    del parts, part
+    return ingest.Corpus(full, None, gwords, np.array(gcounts, dtype=np.int64), sent_len=2)
+
+
 MERGE_RULES = {"touch": 0, "mean": 1}  # == G2V_MERGE_TOUCH / G2V_MERGE_MEAN
 
 

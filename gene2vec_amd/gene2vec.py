@@ -259,6 +259,7 @@ def main(argv=None):
     rng = random.Random(args.shuffle_seed) if args.shuffle_seed is not None else random
     corpus = None
     pipe = None
+    n_lines = None
     with ph("ingest"):
         if args.native_ingest:
             files = os.listdir(source_dir)
@@ -266,14 +267,21 @@ def main(argv=None):
             paths = [os.path.join(source_dir, f) for f in files if f.endswith(ending_pattern)]
             print(datetime.datetime.now())
             print(f"native ingest of {len(paths)} files")
-            # the shuffles depend only on the pair count and rng: start drawing
-            # the first one (src/gene2vec.py:52) from a newline count while the
-            # files are tokenised
-            n_lines = ingest.count_lines(paths)
             if shuffle_mode == "python":
+                # the shuffles depend only on the pair count and rng: start
+                # drawing the first one (src/gene2vec.py:52) from a newline
+                # count while the files are tokenised
+                n_lines = ingest.count_lines(paths)
                 pipe = ingest.ShufflePipeline(n_lines, rng, max(1, args.iters))
             try:
-                corpus = ingest.read_corpus(paths)
+                if world > 1 and shuffle_mode == "device":
+                    # each rank tokenises its own range of the files; the ranks
+                    # then share the tokens (None: not all pairs -> every rank
+                    # reads everything)
+                    from . import distributed as Dd
+                    corpus = Dd.gather_corpus(paths)
+                if corpus is None:
+                    corpus = ingest.read_corpus(paths)
             except BaseException:
                 if pipe is not None:
                     pipe.close(wait=True)
@@ -304,7 +312,7 @@ def main(argv=None):
         elif corpus is not None:
             # this shuffle and the reshuffle before every later iteration (:80)
             # are drawn ahead on host threads while the GPU trains
-            if corpus.n_sent != n_lines:  # cannot happen; never shuffle the wrong n
+            if n_lines is not None and corpus.n_sent != n_lines:  # never shuffle the wrong n
                 pipe.close(wait=True)
                 pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
             perm = pipe.next()

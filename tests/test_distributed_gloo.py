@@ -189,3 +189,67 @@ def test_single_process_trainer_never_merges():
     tr = Dd.ReplicaTrainer(eng, t, avg_every_jobs=3, merge="touch")
     tr.train_epoch(np.arange(0, 15, 2, dtype=np.int64), np.zeros(7), np.zeros(7, np.uint64))
     assert tr.averages == 0 and len(eng.calls) == 3
+
+
+def _gather_worker(rank, world, port, paths, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = Dd.gather_corpus(paths)
+        q.put((rank, None if c is None else (c.tokens.copy(), list(c.words), c.counts.copy(),
+                                             c.n_sent, c.pairs_only)))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_gather(paths, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, paths, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _write_pairs(d, k, pairs, names):
+    p = d / f"pairs_{k}.txt"
+    p.write_text("\n".join(f"{names[a]} {names[b]}" for a, b in pairs) + "\n",
+                 encoding="windows-1252")
+    return str(p)
+
+
+@pytest.mark.parametrize("world,n_files", [(2, 3), (3, 2)])
+def test_gather_corpus_equals_single_reader(tmp_path, world, n_files):
+    """rank-sharded ingest (each rank tokenises its file range, the ranks share
+    words and tokens) builds the single-process reader's corpus on every rank;
+    with more ranks than files a rank reads nothing and still takes part"""
+    from gene2vec_amd import ingest
+    names = S.gene_names(300)
+    pairs = S.zipf_gene_pairs(3000, 300, 1.0, seed=5)
+    paths = [_write_pairs(tmp_path, k, part, names)
+             for k, part in enumerate(np.array_split(pairs, n_files))]
+    ref = ingest.read_corpus(paths)
+    res = _run_gather(paths, world)
+    for r in range(world):
+        tok, words, counts, n_sent, pairs_only = res[r]
+        assert words == list(ref.words)
+        assert np.array_equal(counts, ref.counts)
+        assert np.array_equal(tok, ref.tokens)
+        assert n_sent == ref.n_sent and pairs_only
+
+
+def test_gather_corpus_declines_non_pairs(tmp_path):
+    names = S.gene_names(50)
+    pairs = S.zipf_gene_pairs(200, 50, 1.0, seed=6)
+    p0 = _write_pairs(tmp_path, 0, pairs, names)
+    p1 = tmp_path / "pairs_1.txt"
+    p1.write_text("G00001 G00002 G00003\n", encoding="windows-1252")
+    res = _run_gather([p0, str(p1)], 2)
+    assert res[0] is None and res[1] is None
