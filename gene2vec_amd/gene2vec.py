@@ -387,8 +387,11 @@ def main(argv=None):
                     # src/gene2vec.py:86 reloads the checkpoint it just saved; the
                     # model kept from the last iteration is that state (save/load
                     # round-trips bit for bit), and its device tables and engine stay
-                    # resident.  Data-parallel ranks take rank 0's checkpoint.
-                    if args.reload_checkpoints or world > 1 or model is None:
+                    # resident.  Data-parallel ranks keep theirs too: the epoch ends
+                    # with a merge, after which every replica holds the same bits
+                    # (one all-reduce result, the same apply kernel), so the engine,
+                    # its RCCL communicator and the merge snapshot carry over.
+                    if args.reload_checkpoints or model is None:
                         model = Word2Vec.load(prev, device=args.device)
                         model.data_parallel = world > 1
                 if corpus is None:
@@ -426,13 +429,17 @@ def main(argv=None):
                 # thread while the next iteration trains (one at a time, in order)
                 # a snapshot: the next iteration rebinds model.wv's arrays
                 exporter.submit(name, copy.copy(model.wv), ph)
-            if world > 1:
+            if world > 1 and args.reload_checkpoints:
                 import torch.distributed as dist
                 dist.barrier()  # the next iteration loads rank 0's checkpoint
             print(f"gene2vec dimension {dimension} iteration {current_iter} done")
             outputs.append(name)
-            if args.reload_checkpoints or world > 1:
+            if args.reload_checkpoints:
                 model = None  # freed (device tables too) before the reload
+        dump = os.environ.get("G2V_DUMP_REPLICA")
+        if dump and model is not None:  # test hook: every rank's final tables
+            model._sync_host()
+            np.savez(f"{dump}_rank{rank}.npz", syn0=model.wv.vectors, syn1neg=model.syn1neg)
     finally:
         if pipe is not None:
             pipe.close(wait=True)

@@ -83,3 +83,33 @@ def test_cli_data_parallel_two_ranks(tmp_path):
     # process on a corpus this small; bar: 93 % of the single run's improvement
     # (measured 2.8221 vs 2.7867 = 97 %)
     assert (init - l2) >= 0.93 * (init - l1), (l1, l2)
+
+
+def test_cli_data_parallel_replicas_identical(tmp_path):
+    """the data-parallel CLI keeps each rank's model between iterations (no
+    checkpoint reload): every epoch ends with a merge, so the replicas must
+    hold the same bits -- every rank writes its final tables here and they
+    are compared"""
+    V, n_pairs = 800, 120_000
+    names = S.gene_names(V)
+    pairs = S.zipf_gene_pairs(n_pairs, V, 1.0, seed=12)
+    data = tmp_path / "data"
+    data.mkdir()
+    for k, part in enumerate(np.array_split(pairs, 3)):
+        (data / f"pairs_{k}.txt").write_text(
+            "\n".join(f"{names[a]} {names[b]}" for a, b in part) + "\n", encoding="windows-1252")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", G2V_DUMP_REPLICA=str(tmp_path / "rep"),
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
+           "--backend", "gloo", "--iters", "3", "--dim", "32", "--hash", "crc32",
+           "--shuffle-seed", "3", "--native-ingest", "--no-txt", "--no-w2v",
+           "--merge-every-jobs", "4"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    a = np.load(str(tmp_path / "rep") + "_rank0.npz")
+    b = np.load(str(tmp_path / "rep") + "_rank1.npz")
+    assert np.array_equal(a["syn0"], b["syn0"]) and np.array_equal(a["syn1neg"], b["syn1neg"])
+    m = Word2Vec.load(str(tmp_path / "dp" / "gene2vec_dim_32_iter_3"))
+    assert np.array_equal(m.wv.vectors, a["syn0"])
