@@ -561,7 +561,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 5, G2V_EINVAL, "debug write mode out of [0, 5]");
+      REQUIRE(value >= 0 && value <= 7, G2V_EINVAL, "debug write mode out of [0, 7]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_ATOMIC_OVERLAP:
@@ -943,7 +943,9 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.V = c->V;
   s.hot_rows = c->hot_rows < 0 ? c->V : std::min(c->hot_rows, c->V);
   s.exp_table = c->exp_table;
-  s.debug_write = c->debug_write;
+  // 6: production writes, 7: scratch atomics (mode 4); both read main rows only
+  s.debug_write = c->debug_write == 6 ? 0 : c->debug_write == 7 ? 4 : c->debug_write;
+  s.skip_copy_reads = c->debug_write >= 6 ? 1 : 0;
   s.compute_loss = closs ? 1 : 0;
   s.log_table = c->log_table;
   s.loss_f64 = c->d_loss;
@@ -972,7 +974,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   const int64_t max_rows2 = kStripeMaxBytes / (2 * 4 * (int64_t)(c->stripe2_copies - 1) * c->ld);
   const int r2 = (int)std::min<int64_t>(std::min(stripe2_rows_eff(c), c->V),
                                         (int64_t)s.stripe_rows + max_rows2);
-  const bool tier2 = striped && c->debug_write == 0 && r2 > s.stripe_rows;
+  const bool tier2 = striped && (c->debug_write == 0 || c->debug_write == 6) && r2 > s.stripe_rows;
   s.stripe2_rows = tier2 ? r2 : s.stripe_rows;
   s.stripe2_copies = tier2 ? c->stripe2_copies : 1;
   if (tier2) {
@@ -983,9 +985,9 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     }
   }
   s.stripe2 = c->stripe2;
-  if (c->debug_write == 3 || c->debug_write == 4) {
+  if (c->debug_write == 3 || c->debug_write == 4 || c->debug_write == 7) {
     const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
-    const int64_t words = rows * c->ld * (c->debug_write == 4 ? 2 : 1);
+    const int64_t words = rows * c->ld * (c->debug_write == 3 ? 1 : 2);
     if ((rc = dev_reserve(c->stream, &c->dbg16, &c->dbg16_cap, words))) return rc;
     HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
   }

@@ -103,6 +103,7 @@ struct SgnsArgs {
   float* stripe2;
   int stripe2_rows;         // <= stripe_rows = off
   int stripe2_copies;
+  int skip_copy_reads;      // ablation (G2V_OPT_DEBUG_WRITE 6): readers ignore stripe copies
   int overlap;              // G2V_OPT_ATOMIC_OVERLAP
   unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]

@@ -149,7 +149,10 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
       for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  const int R1 = a.stripe_rows, R2 = a.stripe2_rows;
+  // ablation 6 (G2V_OPT_DEBUG_WRITE): copies are written but not read (the
+  // throughput a drained-copy design would have; values go stale)
+  const int R1 = a.skip_copy_reads ? 0 : a.stripe_rows;
+  const int R2 = a.skip_copy_reads ? 0 : a.stripe2_rows;
   if (x.input < R1)
     add_stripes<NV>(x.l1, rs, x.input, 0, R1, a.stripe_copies, rowb, loff);
   else if (x.input < R2)

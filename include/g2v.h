@@ -115,7 +115,9 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
  *                         atomics, 2 no table writes, 3 packed-f16 / 4 f32
  *                         atomics into a scratch table, 5 syn1neg atomics only
- *                         (syn0 never written) [0]
+ *                         (syn0 never written), 6 stripe copies written but
+ *                         never read (readers see main rows only), 7 = 4 with
+ *                         main-row-only reads [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE2_ROWS  second stripe tier: rows [STRIPE_ROWS, this) get
  *                         STRIPE2_COPIES copies each (<= STRIPE_ROWS = off);
