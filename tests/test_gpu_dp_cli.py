@@ -113,3 +113,31 @@ def test_cli_data_parallel_replicas_identical(tmp_path):
     assert np.array_equal(a["syn0"], b["syn0"]) and np.array_equal(a["syn1neg"], b["syn1neg"])
     m = Word2Vec.load(str(tmp_path / "dp" / "gene2vec_dim_32_iter_3"))
     assert np.array_equal(m.wv.vectors, a["syn0"])
+
+
+def test_cli_data_parallel_ragged_corpus_falls_back(tmp_path):
+    """a corpus with lines that are not pairs (the generator's 4-token lines
+    at study boundaries) cannot take the device shuffles: under
+    torchrun every rank then reads every file and shuffles with Python's
+    random (seeded alike), and training still runs data-parallel"""
+    V = 300
+    names = S.gene_names(V)
+    pairs = S.zipf_gene_pairs(40_000, V, 1.0, seed=14)
+    data = tmp_path / "data"
+    data.mkdir()
+    lines = [f"{names[a]} {names[b]}" for a, b in pairs]
+    lines[100] = lines[100] + " " + lines[101]  # one 4-token sentence
+    (data / "pairs_0.txt").write_text("\n".join(lines[:20000]) + "\n", encoding="windows-1252")
+    (data / "pairs_1.txt").write_text("\n".join(lines[20000:]) + "\n", encoding="windows-1252")
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
+           "--backend", "gloo", "--iters", "2", "--dim", "16", "--hash", "crc32",
+           "--shuffle-seed", "2", "--native-ingest", "--no-txt", "--no-w2v"]
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "using Python's shuffle" in r.stdout
+    m = Word2Vec.load(str(tmp_path / "dp" / "gene2vec_dim_16_iter_2"))
+    assert m.corpus_count == 40_000 and np.isfinite(m.wv.vectors).all()
