@@ -84,3 +84,27 @@ def test_first_occurrence_matches_oracle(n, n_ids):
         E.first_occurrence_perm8(0, src.data_ptr(), n, seed, n_ids, first.data_ptr())
         torch.cuda.synchronize()
         assert np.array_equal(first.cpu().numpy(), S.first_occurrence(pairs, seed, n_ids))
+
+
+def test_gpu_matches_committed_anchors():
+    """g2v_permute_items8 / g2v_first_occurrence_perm8 against the committed
+    anchors (tests/golden/device_shuffle.json) for every case that fits"""
+    import json
+    import os
+
+    import torch
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "device_shuffle.json")))
+    for c in g["cases"]:
+        if c["n"] > 100_000_000:
+            continue
+        src = torch.arange(c["n"], dtype=torch.int64, device="cuda:0")
+        for i, want in zip(c["idx"], c["perm"]):
+            assert int(_perm(src, c["n"], i, 1, c["seed"])[0].item()) == want, c
+    fo = g["first_occurrence"]
+    pairs = np.array(fo["pairs"], np.int32)
+    first = torch.empty(fo["n_ids"], dtype=torch.int64, device="cuda:0")
+    items = _dev(pairs.view(np.int64).reshape(-1))  # kept alive until the sync
+    E.first_occurrence_perm8(0, items.data_ptr(), len(pairs), fo["seed"], fo["n_ids"],
+                             first.data_ptr())
+    torch.cuda.synchronize()
+    assert first.cpu().tolist() == fo["first"]

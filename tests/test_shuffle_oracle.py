@@ -43,3 +43,17 @@ def test_uniform_positions():
     # neighbours stay apart: consecutive outputs are not consecutive inputs
     p = S.perm_at(100_000, 9, np.arange(100_000, dtype=np.uint64))
     assert np.mean(np.abs(np.diff(p)) == 1) < 1e-3
+
+
+def test_matches_committed_anchors():
+    """the restated permutation equals the committed anchors (including a
+    2^40-item domain: 21-bit halves, cycle-walking at scale)"""
+    import json
+    import os
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "device_shuffle.json")))
+    for c in g["cases"]:
+        got = S.perm_at(c["n"], c["seed"], np.array(c["idx"], np.uint64))
+        assert [int(v) for v in got] == c["perm"], c
+    fo = g["first_occurrence"]
+    assert [int(v) for v in S.first_occurrence(np.array(fo["pairs"], np.int32), fo["seed"],
+                                               fo["n_ids"])] == fo["first"]
