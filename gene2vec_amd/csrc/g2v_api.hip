@@ -557,7 +557,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe2_copies = (int)value;
       return G2V_OK;
     case G2V_OPT_STRIPE_COPIES:
-      REQUIRE(value >= 0 && value <= 16, G2V_EINVAL, "stripe copies out of [0, 16]");
+      REQUIRE(value >= 0 && value <= 32, G2V_EINVAL, "stripe copies out of [0, 32]");
       c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
