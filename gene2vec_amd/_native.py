@@ -19,7 +19,7 @@ G2V_ENOMEM = -3
 G2V_ESTATE = -4
 G2V_ERANGE = -5
 G2V_ECOMM = -6
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
@@ -44,6 +44,9 @@ OPT_MERGE_EVERY_JOBS = 11
 OPT_MERGE_RULE = 12
 OPT_STRIPE2_ROWS = 13
 OPT_STRIPE2_COPIES = 14
+OPT_ACTIVE_WAVES = 15
+COLL_SUM = 0
+COLL_BCAST0 = 1
 BATCH_WORDS = 10000
 MAX_DIM = 512
 TXT_MATRIX = 0
@@ -65,7 +68,9 @@ class Stats(C.Structure):
     _fields_ = [("raw_words", C.c_int64), ("effective_words", C.c_int64),
                 ("examples", C.c_int64), ("jobs", C.c_int64), ("launches", C.c_int64),
                 ("sgns_kernel_ms", C.c_double), ("sample_kernel_ms", C.c_double),
-                ("training_loss", C.c_double)]
+                ("training_loss", C.c_double), ("sgns_grid", C.c_int64),
+                ("stripe_rows", C.c_int64), ("stripe_copies", C.c_int64),
+                ("stripe2_rows", C.c_int64), ("stripe2_copies", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -77,6 +82,8 @@ _i64 = C.c_int64
 _u32 = C.c_uint32
 _f32 = C.c_float
 _f64 = C.c_double
+# g2v_collective_fn: int (*)(void *user, int op, float *buf, int64_t count)
+COLLECTIVE_FN = C.CFUNCTYPE(C.c_int, _vp, C.c_int, C.POINTER(C.c_float), _i64)
 
 # name -> (restype, argtypes); every symbol include/g2v.h declares
 SIGNATURES = {
@@ -104,6 +111,11 @@ SIGNATURES = {
     "g2v_average": (C.c_int, [_vp, C.c_int]),
     "g2v_merge_snapshot": (C.c_int, [_vp]),
     "g2v_average_local": (C.c_int, [C.POINTER(_vp), C.c_int, C.c_int]),
+    "g2v_local_group_create": (C.c_int, [C.c_int, C.c_int, C.POINTER(_vp)]),
+    "g2v_local_group_destroy": (C.c_int, [_vp]),
+    "g2v_comm_init_local": (C.c_int, [_vp, _vp, C.c_int]),
+    "g2v_comm_init_host": (C.c_int, [_vp, COLLECTIVE_FN, _vp, C.c_int, C.c_int]),
+    "g2v_comm_abort": (C.c_int, [_vp]),
     "g2v_read_stats": (C.c_int, [_vp, C.POINTER(Stats)]),
     "g2v_cosine_pairs": (C.c_int, [C.c_int, _vp, _i64, _i32, _vp, _vp, _i64, _vp]),
     "g2v_permute_items8": (C.c_int, [C.c_int, _vp, _vp, _i64, _i64, _i64, C.c_uint64, _vp]),

@@ -13,6 +13,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -93,6 +96,34 @@ int g2v::set_error(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+
+enum { kCommNone = 0, kCommRccl = 1, kCommLocal = 2, kCommHost = 3 };
+
+// In-process replica group (g2v_comm_init_local): n contexts of one process on
+// one device, each driven by its own host thread, merge through a device sum
+// instead of ncclAllReduce -- the RCCL path's delta/apply kernels and in-call
+// merges with several replicas on a one-GPU box, where RCCL refuses two ranks
+// ("Duplicate GPU detected").  Collectives meet at a host barrier; the data
+// dependencies between the ranks' streams are HIP events.
+struct g2v_local_group {
+  int n = 0;
+  int device = -1;
+  int32_t V = 0;
+  int64_t ld = 0;
+  int timeout_s = 600;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool aborted = false;
+  std::string why;
+  std::vector<int> joined;
+  std::vector<hipEvent_t> ev;                 // per rank: its buffers are ready
+  hipEvent_t ev_done = nullptr;               // rank 0: the sum is in scratch
+  std::vector<std::array<float*, 3>> bufs;    // per rank: the buffers of this collective
+  float* scratch = nullptr;
+  size_t scratch_cap = 0;                     // floats
+};
 
 struct g2v_ctx {
   int device = 0;
@@ -184,8 +215,20 @@ struct g2v_ctx {
   float *merge0 = nullptr, *merge1 = nullptr, *merge_cnt = nullptr;
   int64_t merge_ld = 0;
   bool merge_valid = false;
+  // the merge's transport: RCCL (g2v_comm_init), an in-process group of
+  // contexts (g2v_comm_init_local) or a host collective callback
+  // (g2v_comm_init_host); the merge kernels are the same for all three
+  int comm_kind = 0;  // kCommNone / kCommRccl / kCommLocal / kCommHost
   ncclComm_t comm = nullptr;
+  g2v_local_group* lgroup = nullptr;
+  g2v_collective_fn host_fn = nullptr;
+  void* host_user = nullptr;
+  float* h_coll = nullptr;  // pinned staging of the host transport
+  size_t h_coll_cap = 0;
   int nranks = 1, rank = 0;
+  int active_waves = 4;  // G2V_OPT_ACTIVE_WAVES
+  int last_grid = 0, last_stripe_rows = 0, last_stripe_copies = 1, last_stripe2_rows = 0,
+      last_stripe2_copies = 1;  // layout of the last Hogwild launch (g2v_stats)
   int64_t jobs = 0, launches = 0;
 
   // timing
@@ -264,6 +307,7 @@ struct Rccl {
   decltype(&ncclGetUniqueId) get_unique_id = nullptr;
   decltype(&ncclCommInitRank) comm_init_rank = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;  // optional
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclBroadcast) broadcast = nullptr;
   decltype(&ncclGroupStart) group_start = nullptr;
@@ -301,6 +345,7 @@ const Rccl& rccl() {
       r.get_unique_id = nullptr;
       r.load_error = "librccl.so.1 lacks an nccl* entry point";
     }
+    r.comm_abort = reinterpret_cast<decltype(&ncclCommAbort)>(dlsym(h, "ncclCommAbort"));
   });
   return r;
 }
@@ -317,9 +362,14 @@ int rccl_fail(ncclResult_t e, const char* what) {
     if (e_ != ncclSuccess) return rccl_fail(e_, what); \
   } while (0)
 
+// leave the current communicator (any transport) in an orderly way
 static void comm_destroy(g2v_ctx* c) {
   if (c->comm && rccl().comm_destroy) (void)rccl().comm_destroy(c->comm);
   c->comm = nullptr;
+  c->comm_kind = 0;
+  c->lgroup = nullptr;
+  c->host_fn = nullptr;
+  c->host_user = nullptr;
   c->nranks = 1;
   c->rank = 0;
 }
@@ -482,6 +532,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->stripe2);
   dev_free(c->dbg16);
   if (c->h_stage) (void)hipHostFree(c->h_stage);
+  if (c->h_coll) (void)hipHostFree(c->h_coll);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->stage_ev) (void)hipEventDestroy(c->stage_ev);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -586,6 +637,11 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->grid_user = value > 0;
       c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv, c->u_max);
       return G2V_OK;
+    case G2V_OPT_ACTIVE_WAVES:
+      REQUIRE(value >= 1 && value <= kSgnsThreads / 64, G2V_EINVAL, "active waves out of [1, %d]",
+              kSgnsThreads / 64);
+      c->active_waves = (int)value;
+      return G2V_OK;
     default:
       return fail(G2V_EINVAL, "unknown option key %d", key);
   }
@@ -607,6 +663,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_SAMPLE_OVERLAP: *out = c->sample_overlap; return G2V_OK;
     case G2V_OPT_MERGE_EVERY_JOBS: *out = c->merge_every; return G2V_OK;
     case G2V_OPT_MERGE_RULE: *out = c->merge_rule; return G2V_OK;
+    case G2V_OPT_ACTIVE_WAVES: *out = c->active_waves; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -680,6 +737,10 @@ int g2v_bind_tables(g2v_ctx* c, float* s0, float* s1, int64_t ld) {
           (long long)ld, c->D);
   REQUIRE(((uintptr_t)s0 % 16) == 0 && ((uintptr_t)s1 % 16) == 0, G2V_EINVAL,
           "tables must be 16-byte aligned");
+  // the update kernels address a table through one buffer resource (32-bit
+  // offsets): rows past 2 GiB would read as zeros and lane offsets would wrap
+  REQUIRE((int64_t)c->V * ld * 4 < ((int64_t)1 << 31), G2V_ERANGE,
+          "vocab_size=%d x ld=%lld exceeds the 2 GiB per-table limit", c->V, (long long)ld);
   c->syn0 = s0;
   c->syn1 = s1;
   c->ld = ld;
@@ -960,6 +1021,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.stripe_rows = striped ? srows : 0;
   s.stripe_copies = striped ? copies : 1;
   s.overlap = c->atomic_overlap;
+  s.active_waves = c->active_waves;
   s.queue = c->d_queue;
   int rc;
   if (striped) {
@@ -1010,11 +1072,21 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipEventRecord(e1, c->stream));
     c->t_sgns.emplace_back(e0, e1);
   }
+  if (atomic_kernel) {
+    c->last_grid = c->sgns_grid;
+    c->last_stripe_rows = s.stripe_rows;
+    c->last_stripe_copies = s.stripe_copies;
+    c->last_stripe2_rows = s.stripe2_rows;
+    c->last_stripe2_copies = s.stripe2_copies;
+  }
   c->launches++;
   return G2V_OK;
 }
 
 static int merge_now(g2v_ctx* c, int rule);
+static int comm_broadcast_tables(g2v_ctx* c);
+static int comm_abort(g2v_ctx* c, const char* why);
+static void group_abort(g2v_local_group* g, const char* why);
 
 extern "C" {
 
@@ -1072,10 +1144,34 @@ int g2v_plan_jobs(const int64_t* sent_off, int64_t n_sent, int64_t sent_len, int
   return G2V_OK;
 }
 
+}  // extern "C"
+
+static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha,
+                      const uint64_t* job_seed, int64_t n_jobs, uint32_t flags);
+
+extern "C" {
+
 int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const uint64_t* job_seed,
               int64_t n_jobs, uint32_t flags) {
   int rc = set_dev(c);
   if (rc) return rc;
+  const bool merging = c->comm_kind != kCommNone && c->merge_every > 0;
+  rc = train_impl(c, job_sent, job_alpha, job_seed, n_jobs, flags);
+  if (rc && merging) {
+    // the peers may already wait in one of this call's merges (or will wait
+    // in the next one): leave the communicator so they fail instead of hanging
+    const std::string msg = g_err;
+    comm_abort(c, msg.c_str());
+    g_err = msg + " (communicator aborted)";
+  }
+  return rc;
+}
+
+}  // extern "C"
+
+static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha,
+                      const uint64_t* job_seed, int64_t n_jobs, uint32_t flags) {
+  int rc;
   REQUIRE(c->vocab_ready, G2V_ESTATE, "g2v_set_vocab must precede g2v_train");
   REQUIRE(c->corpus_ready, G2V_ESTATE, "g2v_set_corpus must precede g2v_train");
   REQUIRE(job_alpha && job_seed, G2V_EINVAL, "job_alpha / job_seed is null");
@@ -1096,7 +1192,7 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
     bool merge;
   };
   std::vector<Seg> segs;
-  const bool merging = c->comm && c->merge_every > 0;
+  const bool merging = c->comm_kind != kCommNone && c->merge_every > 0;
   const int64_t win = merging ? c->merge_every : n_jobs;
   for (int64_t w0 = 0; w0 < n_jobs; w0 += win) {
     const int64_t w1 = std::min<int64_t>(n_jobs, w0 + win);
@@ -1149,6 +1245,8 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
   c->jobs += n_jobs;
   return G2V_OK;
 }
+
+extern "C" {
 
 int g2v_debug_sample(g2v_ctx* c, const int64_t* job_sent, const uint64_t* job_seed, int64_t n_jobs,
                      int32_t* rec_out, int64_t cap, int64_t* n_out) {
@@ -1328,6 +1426,11 @@ int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
   out->raw_words = (int64_t)cnt[2];
   out->jobs = c->jobs;
   out->launches = c->launches;
+  out->sgns_grid = c->last_grid;
+  out->stripe_rows = c->last_stripe_rows;
+  out->stripe_copies = c->last_stripe_copies;
+  out->stripe2_rows = c->last_stripe2_rows;
+  out->stripe2_copies = c->last_stripe2_copies;
   for (auto& p : c->t_sgns) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));
@@ -1398,37 +1501,328 @@ int g2v_comm_init(g2v_ctx* c, const void* id, int nranks, int rank) {
   ncclComm_t comm = nullptr;
   NCCLCHK(r.comm_init_rank(&comm, nranks, uid, rank), "ncclCommInitRank");
   c->comm = comm;
+  c->comm_kind = kCommRccl;
   c->nranks = nranks;
   c->rank = rank;
-  // every replica starts from rank 0's tables (Python's hash() seeds the
-  // reference's init differently in every process)
-  const size_t tab = (size_t)c->V * (size_t)c->ld;
-  if (nranks > 1) {
-    NCCLCHK(r.group_start(), "ncclGroupStart");
-    NCCLCHK(r.broadcast(c->syn0, c->syn0, tab, ncclFloat32, 0, comm, c->stream), "ncclBroadcast");
-    NCCLCHK(r.broadcast(c->syn1, c->syn1, tab, ncclFloat32, 0, comm, c->stream), "ncclBroadcast");
-    NCCLCHK(r.group_end(), "ncclGroupEnd");
-  }
+  if ((rc = comm_broadcast_tables(c))) return rc;
   return g2v_merge_snapshot(c);
+}
+
+int g2v_local_group_create(int nranks, int timeout_s, g2v_local_group** out) {
+  REQUIRE(out != nullptr, G2V_EINVAL, "out is null");
+  *out = nullptr;
+  REQUIRE(nranks >= 1 && nranks <= kMaxLocalReplicas, G2V_EINVAL, "nranks %d out of [1, %d]",
+          nranks, kMaxLocalReplicas);
+  REQUIRE(timeout_s >= 0, G2V_EINVAL, "timeout_s < 0");
+  g2v_local_group* g = new (std::nothrow) g2v_local_group();
+  REQUIRE(g != nullptr, G2V_ENOMEM, "group allocation failed");
+  g->n = nranks;
+  g->timeout_s = timeout_s ? timeout_s : 600;
+  g->joined.assign((size_t)nranks, 0);
+  g->ev.assign((size_t)nranks, nullptr);
+  g->bufs.assign((size_t)nranks, {nullptr, nullptr, nullptr});
+  *out = g;
+  return G2V_OK;
+}
+
+int g2v_local_group_destroy(g2v_local_group* g) {
+  if (!g) return G2V_OK;
+  if (g->device >= 0) (void)hipSetDevice(g->device);
+  (void)hipDeviceSynchronize();
+  for (hipEvent_t e : g->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (g->ev_done) (void)hipEventDestroy(g->ev_done);
+  dev_free(g->scratch);
+  delete g;
+  return G2V_OK;
+}
+
+int g2v_comm_init_local(g2v_ctx* c, g2v_local_group* g, int rank) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(g != nullptr, G2V_EINVAL, "group is null");
+  REQUIRE(rank >= 0 && rank < g->n, G2V_EINVAL, "rank %d of %d invalid", rank, g->n);
+  REQUIRE(c->weights_ready, G2V_ESTATE, "set or bind the tables before g2v_comm_init_local");
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->device < 0) {
+      g->device = c->device;
+      g->V = c->V;
+      g->ld = c->ld;
+    }
+    if (g->device != c->device || g->V != c->V || g->ld != c->ld) {
+      g->aborted = true;
+      g->why = "ranks differ in device / V / ld";
+      g->cv.notify_all();
+      return fail(G2V_EINVAL, "rank %d: device / V / ld differ from the group's", rank);
+    }
+    REQUIRE(!g->joined[(size_t)rank], G2V_EINVAL, "rank %d joined twice", rank);
+    g->joined[(size_t)rank] = 1;
+    if (!g->ev[(size_t)rank])
+      HIPCHK(hipEventCreateWithFlags(&g->ev[(size_t)rank], hipEventDisableTiming));
+    if (rank == 0) {
+      HIPCHK(hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming));
+      // both tables and both touched-count vectors of one merge
+      const size_t need = 2 * (size_t)c->V * (size_t)c->ld + 2 * (size_t)c->V;
+      if ((rc = dev_alloc(&g->scratch, need))) return rc;
+      g->scratch_cap = need;
+    }
+  }
+  comm_destroy(c);
+  c->lgroup = g;
+  c->comm_kind = kCommLocal;
+  c->nranks = g->n;
+  c->rank = rank;
+  if ((rc = comm_broadcast_tables(c))) return rc;
+  return g2v_merge_snapshot(c);
+}
+
+int g2v_comm_init_host(g2v_ctx* c, g2v_collective_fn fn, void* user, int nranks, int rank) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(fn != nullptr, G2V_EINVAL, "collective callback is null");
+  REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, G2V_EINVAL, "rank %d of %d invalid", rank,
+          nranks);
+  REQUIRE(c->weights_ready, G2V_ESTATE, "set or bind the tables before g2v_comm_init_host");
+  comm_destroy(c);
+  c->host_fn = fn;
+  c->host_user = user;
+  c->comm_kind = kCommHost;
+  c->nranks = nranks;
+  c->rank = rank;
+  if ((rc = comm_broadcast_tables(c))) return rc;
+  return g2v_merge_snapshot(c);
+}
+
+int g2v_comm_abort(g2v_ctx* c) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  return comm_abort(c, "g2v_comm_abort");
 }
 
 int g2v_average(g2v_ctx* c, int rule) {
   int rc = set_dev(c);
   if (rc) return rc;
   REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %d", rule);
-  if (!c->comm) return G2V_OK;  // no communicator: nothing to merge with
-  return merge_now(c, rule);
+  if (c->comm_kind == kCommNone) return G2V_OK;  // no communicator: nothing to merge with
+  rc = merge_now(c, rule);
+  if (rc) {
+    const std::string msg = g_err;
+    comm_abort(c, msg.c_str());
+    g_err = msg + " (communicator aborted)";
+  }
+  return rc;
 }
 
 }  // extern "C"
+
+// ---- transports -------------------------------------------------------------------
+// a failing rank aborts the in-process group so its peers do not wait forever
+#define GCHK(x)                                       \
+  do {                                                \
+    const int rc_ = (x);                              \
+    if (rc_) {                                        \
+      group_abort(g, g_err.c_str());                  \
+      return rc_;                                     \
+    }                                                 \
+  } while (0)
+#define GHIP(x)                                                                      \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      const int rc_ = fail(G2V_EHIP, "%s failed: %s", #x, hipGetErrorString(e_));    \
+      group_abort(g, g_err.c_str());                                                 \
+      return rc_;                                                                    \
+    }                                                                                \
+  } while (0)
+
+static void group_abort(g2v_local_group* g, const char* why) {
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (!g->aborted) {
+    g->aborted = true;
+    g->why = why ? why : "?";
+  }
+  g->cv.notify_all();
+}
+
+// host barrier of the group's ranks (a collective's meeting point)
+static int group_wait(g2v_local_group* g) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  if (g->aborted) return fail(G2V_ECOMM, "replica group aborted: %s", g->why.c_str());
+  const uint64_t my = g->gen;
+  if (++g->arrived == g->n) {
+    g->arrived = 0;
+    ++g->gen;
+    g->cv.notify_all();
+    return G2V_OK;
+  }
+  const bool done = g->cv.wait_for(lk, std::chrono::seconds(g->timeout_s),
+                                   [&] { return g->gen != my || g->aborted; });
+  if (g->gen != my) return G2V_OK;
+  if (!done && !g->aborted) {
+    g->aborted = true;
+    g->why = "a rank did not reach the barrier within the timeout";
+    g->cv.notify_all();
+  }
+  return fail(G2V_ECOMM, "replica group aborted: %s", g->why.c_str());
+}
+
+// in place: bufs[b][0, n[b]) <- sum over the group's ranks
+static int local_allreduce(g2v_ctx* c, float* const* bufs, const size_t* n, int nb) {
+  g2v_local_group* g = c->lgroup;
+  const int r = c->rank;
+  size_t total = 0;
+  for (int b = 0; b < nb; ++b) total += n[b];
+  if (total > g->scratch_cap) {
+    const int rc = fail(G2V_EINVAL, "collective of %zu floats exceeds the group's %zu", total,
+                        g->scratch_cap);
+    group_abort(g, g_err.c_str());
+    return rc;
+  }
+  for (int b = 0; b < nb; ++b) g->bufs[(size_t)r][(size_t)b] = bufs[b];
+  GHIP(hipEventRecord(g->ev[(size_t)r], c->stream));  // this rank's inputs are ready
+  GCHK(group_wait(g));
+  if (r == 0) {
+    for (int q = 0; q < g->n; ++q) GHIP(hipStreamWaitEvent(c->stream, g->ev[(size_t)q], 0));
+    size_t off = 0;
+    for (int b = 0; b < nb; ++b) {
+      SumArgs sa{};
+      for (int q = 0; q < g->n; ++q) sa.src[q] = g->bufs[(size_t)q][(size_t)b];
+      GHIP(launch_sum_replicas(sa, g->n, g->scratch + off, (int64_t)n[b], c->stream));
+      off += n[b];
+    }
+    GHIP(hipEventRecord(g->ev_done, c->stream));
+  }
+  GCHK(group_wait(g));
+  // the next collective's sum waits for these copies (it waits for every
+  // rank's next ready event, recorded after them on the rank's stream)
+  if (r != 0) GHIP(hipStreamWaitEvent(c->stream, g->ev_done, 0));
+  size_t off = 0;
+  for (int b = 0; b < nb; ++b) {
+    GHIP(hipMemcpyAsync(bufs[b], g->scratch + off, n[b] * sizeof(float), hipMemcpyDeviceToDevice,
+                        c->stream));
+    off += n[b];
+  }
+  return G2V_OK;
+}
+
+// in place: bufs[b] <- rank 0's bufs[b]
+static int local_broadcast(g2v_ctx* c, float* const* bufs, const size_t* n, int nb) {
+  g2v_local_group* g = c->lgroup;
+  const int r = c->rank;
+  for (int b = 0; b < nb; ++b) g->bufs[(size_t)r][(size_t)b] = bufs[b];
+  GHIP(hipEventRecord(g->ev[(size_t)r], c->stream));
+  GCHK(group_wait(g));
+  if (r != 0) {
+    GHIP(hipStreamWaitEvent(c->stream, g->ev[0], 0));
+    for (int b = 0; b < nb; ++b)
+      GHIP(hipMemcpyAsync(bufs[b], g->bufs[0][(size_t)b], n[b] * sizeof(float),
+                          hipMemcpyDeviceToDevice, c->stream));
+    GHIP(hipEventRecord(g->ev[(size_t)r], c->stream));
+  }
+  GCHK(group_wait(g));
+  // rank 0's tables change again only after every copy of them was taken
+  if (r == 0)
+    for (int q = 1; q < g->n; ++q) GHIP(hipStreamWaitEvent(c->stream, g->ev[(size_t)q], 0));
+  return G2V_OK;
+}
+
+// host transport: device -> pinned host, the caller's collective, back
+static int host_collective(g2v_ctx* c, int op, float* const* bufs, const size_t* n, int nb) {
+  size_t total = 0;
+  for (int b = 0; b < nb; ++b) total += n[b];
+  if (total > c->h_coll_cap) {
+    if (c->h_coll) HIPCHK(hipHostFree(c->h_coll));
+    c->h_coll = nullptr;
+    c->h_coll_cap = 0;
+    HIPCHK(hipHostMalloc((void**)&c->h_coll, total * sizeof(float), hipHostMallocDefault));
+    c->h_coll_cap = total;
+  }
+  size_t off = 0;
+  for (int b = 0; b < nb; ++b) {
+    HIPCHK(hipMemcpyAsync(c->h_coll + off, bufs[b], n[b] * sizeof(float), hipMemcpyDeviceToHost,
+                          c->stream));
+    off += n[b];
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));
+  const int e = c->host_fn(c->host_user, op, c->h_coll, (int64_t)total);
+  REQUIRE(e == 0, G2V_ECOMM, "host collective callback (op %d, %zu floats) returned %d", op, total,
+          e);
+  off = 0;
+  for (int b = 0; b < nb; ++b) {
+    HIPCHK(hipMemcpyAsync(bufs[b], c->h_coll + off, n[b] * sizeof(float), hipMemcpyHostToDevice,
+                          c->stream));
+    off += n[b];
+  }
+  HIPCHK(hipStreamSynchronize(c->stream));  // the staging is reused by the next collective
+  return G2V_OK;
+}
+
+// every replica starts from rank 0's tables (Python's hash() seeds the
+// reference's init differently in every process)
+static int comm_broadcast_tables(g2v_ctx* c) {
+  if (c->nranks <= 1) return G2V_OK;
+  const size_t tab = (size_t)c->V * (size_t)c->ld;
+  float* bufs[2] = {c->syn0, c->syn1};
+  const size_t n[2] = {tab, tab};
+  switch (c->comm_kind) {
+    case kCommRccl: {
+      const Rccl& r = rccl();
+      NCCLCHK(r.group_start(), "ncclGroupStart");
+      for (int k = 0; k < 2; ++k)
+        NCCLCHK(r.broadcast(bufs[k], bufs[k], tab, ncclFloat32, 0, c->comm, c->stream),
+                "ncclBroadcast");
+      NCCLCHK(r.group_end(), "ncclGroupEnd");
+      return G2V_OK;
+    }
+    case kCommLocal: return local_broadcast(c, bufs, n, 2);
+    case kCommHost: return host_collective(c, G2V_COLL_BCAST0, bufs, n, 2);
+    default: return fail(G2V_ESTATE, "no communicator");
+  }
+}
+
+// in place: bufs[b] <- sum over ranks (one grouped collective)
+static int comm_allreduce(g2v_ctx* c, float* const* bufs, const size_t* n, int nb) {
+  switch (c->comm_kind) {
+    case kCommRccl: {
+      const Rccl& r = rccl();
+      NCCLCHK(r.group_start(), "ncclGroupStart");
+      for (int b = 0; b < nb; ++b)
+        NCCLCHK(r.all_reduce(bufs[b], bufs[b], n[b], ncclFloat32, ncclSum, c->comm, c->stream),
+                "ncclAllReduce");
+      NCCLCHK(r.group_end(), "ncclGroupEnd");
+      return G2V_OK;
+    }
+    case kCommLocal: return local_allreduce(c, bufs, n, nb);
+    case kCommHost: return host_collective(c, G2V_COLL_SUM, bufs, n, nb);
+    default: return fail(G2V_ESTATE, "no communicator");
+  }
+}
+
+static int comm_abort(g2v_ctx* c, const char* why) {
+  if (c->comm_kind == kCommRccl && c->comm) {
+    const Rccl& r = rccl();
+    if (r.comm_abort) (void)r.comm_abort(c->comm);
+    else if (r.comm_destroy) (void)r.comm_destroy(c->comm);
+    c->comm = nullptr;
+  } else if (c->comm_kind == kCommLocal && c->lgroup) {
+    group_abort(c->lgroup, why);
+  }
+  c->comm_kind = kCommNone;
+  c->lgroup = nullptr;
+  c->host_fn = nullptr;
+  c->host_user = nullptr;
+  c->nranks = 1;
+  c->rank = 0;
+  return G2V_OK;
+}
 
 // the merge of g2v_average on the context's stream (also run inside g2v_train
 // at G2V_OPT_MERGE_EVERY_JOBS window ends); a one-rank communicator runs the
 // full path, an identity on the values
 static int merge_now(g2v_ctx* c, int rule) {
   REQUIRE(c->merge_valid && c->merge_ld == c->ld, G2V_ESTATE,
-          "no merge snapshot (g2v_comm_init / g2v_merge_snapshot)");
-  const Rccl& r = rccl();
+          "no merge snapshot (g2v_comm_init* / g2v_merge_snapshot)");
   const size_t tab = (size_t)c->V * (size_t)c->ld;
   float* t[2] = {c->syn0, c->syn1};
   float* o[2] = {c->merge0, c->merge1};
@@ -1436,15 +1830,10 @@ static int merge_now(g2v_ctx* c, int rule) {
     for (int k = 0; k < 2; ++k)
       HIPCHK(launch_merge_delta(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
                                 c->stream));
-  NCCLCHK(r.group_start(), "ncclGroupStart");
-  for (int k = 0; k < 2; ++k)
-    NCCLCHK(r.all_reduce(t[k], t[k], tab, ncclFloat32, ncclSum, c->comm, c->stream),
-            "ncclAllReduce");
-  if (rule == G2V_MERGE_TOUCH)
-    NCCLCHK(r.all_reduce(c->merge_cnt, c->merge_cnt, 2 * (size_t)c->V, ncclFloat32, ncclSum,
-                         c->comm, c->stream),
-            "ncclAllReduce");
-  NCCLCHK(r.group_end(), "ncclGroupEnd");
+  float* bufs[3] = {t[0], t[1], c->merge_cnt};
+  const size_t n[3] = {tab, tab, 2 * (size_t)c->V};
+  int rc = comm_allreduce(c, bufs, n, rule == G2V_MERGE_TOUCH ? 3 : 2);
+  if (rc) return rc;
   for (int k = 0; k < 2; ++k)
     HIPCHK(launch_merge_apply(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
                               rule, 1.0f / (float)c->nranks, c->stream));

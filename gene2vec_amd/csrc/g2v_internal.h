@@ -105,6 +105,7 @@ struct SgnsArgs {
   int stripe2_copies;
   int skip_copy_reads;      // ablation (G2V_OPT_DEBUG_WRITE 6): readers ignore stripe copies
   int overlap;              // G2V_OPT_ATOMIC_OVERLAP
+  int active_waves;         // G2V_OPT_ACTIVE_WAVES: waves per workgroup that train (1..4)
   unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
@@ -154,6 +155,13 @@ hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V,
                               int nvec, int rule, float inv_n, hipStream_t st);
 hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
                               int rule, hipStream_t st);
+// in-process replica group (g2v_comm_init_local): dst = sum over n sources,
+// added in source order from 0.f (k_merge_local's order)
+struct SumArgs {
+  const float* src[kMaxLocalReplicas];
+};
+hipError_t launch_sum_replicas(const SumArgs& a, int n, float* dst, int64_t count,
+                               hipStream_t st);
 hipError_t launch_cosine_pairs(const float* v, int64_t V, int D, float* u, const int32_t* a,
                                const int32_t* b, int64_t n, float* out, hipStream_t st);
 // Keyed pseudo-random permutation of [0, n) (the device reshuffle of the

@@ -461,6 +461,50 @@ __global__ __launch_bounds__(256) void k_merge_local(LocalMergeArgs a, int n, in
   }
 }
 
+// the in-process transport's all-reduce (g2v_comm_init_local): dst = sum of n
+// replicas' buffers, added in rank order from 0.f -- the order k_merge_local
+// sums its deltas in, so a merge over the group equals g2v_average_local's bit
+// for bit.  HBM-bound streaming, float4 when every pointer allows it.
+template <bool VEC>
+__global__ __launch_bounds__(256) void k_sum_replicas(SumArgs a, int n, float* __restrict__ dst,
+                                                      int64_t count) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  if (VEC) {
+    const int64_t n4 = count >> 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < n; ++q) {
+        const float4 x = reinterpret_cast<const float4*>(a.src[q])[i];
+        s.x += x.x;
+        s.y += x.y;
+        s.z += x.z;
+        s.w += x.w;
+      }
+      reinterpret_cast<float4*>(dst)[i] = s;
+    }
+  } else {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+      float s = 0.f;
+      for (int q = 0; q < n; ++q) s += a.src[q][i];
+      dst[i] = s;
+    }
+  }
+}
+
+hipError_t launch_sum_replicas(const SumArgs& a, int n, float* dst, int64_t count,
+                               hipStream_t st) {
+  if (count <= 0 || n <= 0) return hipSuccess;
+  bool vec = count % 4 == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+  for (int q = 0; q < n; ++q) vec = vec && (reinterpret_cast<uintptr_t>(a.src[q]) & 15) == 0;
+  const int64_t items = vec ? count / 4 : count;
+  const unsigned grid = (unsigned)std::min<int64_t>((items + 255) / 256, 4096);
+  if (vec)
+    hipLaunchKernelGGL(k_sum_replicas<true>, dim3(grid), dim3(256), 0, st, a, n, dst, count);
+  else
+    hipLaunchKernelGGL(k_sum_replicas<false>, dim3(grid), dim3(256), 0, st, a, n, dst, count);
+  return hipGetLastError();
+}
+
 hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V, int64_t ld,
                               int nvec, hipStream_t st) {
   if (V <= 0) return hipSuccess;

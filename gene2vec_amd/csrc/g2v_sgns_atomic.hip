@@ -244,6 +244,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // G2V_OPT_ACTIVE_WAVES (parity checks): with 1 wave on a 1-workgroup grid the
+  // chunks train in record order and the update order is a fixed function of
+  // the records, restated in oracle/sgns_oracle.c (oracle_atomic_one_wave)
+  if (wid >= a.active_waves) return;
   const int64_t E = *a.n_examples;
   const int D = a.D;
   const int64_t tbytes = (int64_t)a.V * a.ld * 4;

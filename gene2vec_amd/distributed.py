@@ -4,13 +4,16 @@ The reference has no distribution (gensim Hogwild threads in one process,
 src/gene2vec.py:59).  Pairs are independent SGNS examples, so the corpus is
 sharded by contiguous pair ranges; every rank keeps a full replica of
 syn0/syn1neg and trains its shard; every ``avg_every_jobs`` gensim jobs the
-replicas are merged.  The production merge runs inside libg2v
-(``g2v_comm_init`` / ``g2v_average``: fused HIP delta/apply kernels around one
-grouped ncclAllReduce over xGMI on the context's stream); torch.distributed
-only bootstraps it (the RCCL unique id, the vocabulary, scalar agreements).
-The ``torch`` merge backend (row-wise merge of torch-bound tables with
-torch.distributed collectives) remains for gloo: CPU tests and rehearsals
-with several ranks sharing one GPU, which RCCL refuses ("Duplicate GPU").
+replicas are merged.  The merge runs inside libg2v (``g2v_average`` and the
+in-call merges of ``g2v_train``: fused HIP delta/apply kernels around one
+grouped all-reduce on the context's stream) over one of three transports:
+RCCL over xGMI (``g2v_comm_init``, production: one GPU per rank),
+``host_collective`` below (``g2v_comm_init_host``: gloo, for rehearsals with
+several ranks sharing one GPU, which RCCL refuses -- "Duplicate GPU") or an
+in-process group of replicas on one GPU (``g2v_comm_init_local``).
+torch.distributed only bootstraps it (the RCCL unique id, the vocabulary,
+scalar agreements).  The ``torch`` merge backend (row-wise merge of
+torch-bound tables with torch.distributed collectives) remains as an option.
 The vocabulary is global: counts are summed and first occurrences reduced
 with MIN over global token positions, so every rank builds the identical
 index order and cum_table.
@@ -105,6 +108,33 @@ def touch_merge_(tensors, olds, beta=1.0, group=None):
         t.copy_(old)
 
 
+def host_collective(group=None):
+    """The collective of g2v_comm_init_host over torch.distributed (gloo):
+    op(COLL_SUM) gathers every rank's buffer and adds them in rank order from
+    zero -- the order of the in-process group's device sum and of
+    g2v_average_local, so the merged bits do not depend on gloo's reduction
+    schedule; op(COLL_BCAST0) takes rank 0's buffer."""
+    import torch
+    import torch.distributed as dist
+
+    from . import _native as N
+
+    def run(op, buf):
+        t = torch.from_numpy(buf)  # shares the pinned staging buffer
+        if op == N.COLL_BCAST0:
+            dist.broadcast(t, src=0, group=group)
+            return
+        if op != N.COLL_SUM:
+            raise ValueError(f"collective op {op}")
+        parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+        dist.all_gather(parts, t, group=group)
+        s = torch.zeros_like(t)
+        for p in parts:
+            s += p
+        t.copy_(s)
+    return run
+
+
 def world_size(group=None):
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized():
@@ -124,6 +154,19 @@ def allreduce_max_int(v, group=None):
         dev = torch.device("cuda", torch.cuda.current_device())
     t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    return int(t.item())
+
+
+def allreduce_min_int(v, group=None):
+    import torch
+    import torch.distributed as dist
+    if world_size(group) == 1:
+        return int(v)
+    dev = "cpu"
+    if dist.get_backend(group) == "nccl":
+        dev = torch.device("cuda", torch.cuda.current_device())
+    t = torch.tensor([int(v)], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
     return int(t.item())
 
 
@@ -194,6 +237,26 @@ def gather_corpus(paths, group=None):
     return ingest.Corpus(full, None, gwords, np.array(gcounts, dtype=np.int64), sent_len=2)
 
 
+class ThreadAgreement:
+    """min over the threads of an in-process replica group (LocalGroup): the
+    window-count and failure agreements ReplicaTrainer makes over the process
+    group, for ranks that are threads of one process"""
+
+    def __init__(self, n):
+        import threading
+        self._b = threading.Barrier(n)
+        self._vals = [None] * n
+
+    def for_rank(self, rank):
+        def agree(v):
+            self._vals[rank] = v
+            self._b.wait()
+            m = min(self._vals)
+            self._b.wait()  # every rank has read before the next round writes
+            return m
+        return agree
+
+
 MERGE_RULES = {"touch": 0, "mean": 1}  # == G2V_MERGE_TOUCH / G2V_MERGE_MEAN
 
 
@@ -202,11 +265,14 @@ class ReplicaTrainer:
     merges the replicas between windows.
 
     engine:  has ``train(job_sent, alpha, seed, mode, timing=..., compute_loss=...)``
-             and, for backend "rccl", ``average(rule)`` (libg2v's g2v_average
-             after g2v_comm_init).
+             and, for backend "libg2v", ``average(rule)`` (libg2v's g2v_average
+             after g2v_comm_init / _init_host / _init_local).
     tables:  backend "torch" only: the torch tensors bound into the engine.
     merge:   "touch" (row-wise, default) or "mean" (plain model averaging).
-    backend: "rccl" (merge inside libg2v) or "torch" (torch.distributed).
+    backend: "libg2v" (merge inside libg2v, whatever its transport; "rccl" is
+             an alias) or "torch" (torch.distributed).
+    world:   ranks merging (default: the process group's size; an in-process
+             replica group passes its own).
 
     Every rank runs the same number of windows, the maximum over ranks (a
     rank out of jobs still joins each merge), so shards whose job counts
@@ -215,8 +281,10 @@ class ReplicaTrainer:
     """
 
     def __init__(self, engine, tables=(), avg_every_jobs=1024, mode=0, merge="touch", beta=1.0,
-                 backend="torch", group=None):
-        if backend not in ("torch", "rccl"):
+                 backend="torch", group=None, world=None, agree=None):
+        if backend == "rccl":
+            backend = "libg2v"
+        if backend not in ("torch", "libg2v"):
             raise ValueError(backend)
         self.engine = engine
         self.tables = list(tables)
@@ -226,6 +294,9 @@ class ReplicaTrainer:
         self.beta = beta
         self.backend = backend
         self.group = group
+        self._world = world
+        # agree(int) -> min over ranks (window counts use the max, as -min(-x))
+        self._agree = agree
         self.olds = ([t.clone() for t in self.tables]
                      if merge == "touch" and backend == "torch" else None)
         self.averages = 0
@@ -233,14 +304,14 @@ class ReplicaTrainer:
     def train_epoch(self, job_sent, alphas, seeds, timing=False, compute_loss=False):
         n_jobs = len(job_sent) - 1
         every = self.avg_every_jobs
-        world = world_size(self.group)
+        world = self._world if self._world is not None else world_size(self.group)
         n_win = (n_jobs + every - 1) // every
         if world > 1:
-            n_win = allreduce_max_int(n_win, self.group)
+            n_win = -self._min(-n_win)
         kw = {"timing": timing}
         if compute_loss:
             kw["compute_loss"] = True
-        if self.backend == "rccl" and world > 1:
+        if self.backend == "libg2v" and world > 1:
             # one g2v_train call for the whole epoch: libg2v merges at the end
             # of every window of `every` jobs on its own stream
             # (G2V_OPT_MERGE_EVERY_JOBS), so the sampler of the next segment
@@ -250,14 +321,26 @@ class ReplicaTrainer:
             own = (n_jobs + every - 1) // every
             self.engine.set_option(N.OPT_MERGE_RULE, MERGE_RULES[self.merge])
             self.engine.set_option(N.OPT_MERGE_EVERY_JOBS, every)
+            err = None
             try:
                 if n_jobs > 0:
                     self.engine.train(job_sent, alphas, seeds, self.mode, **kw)
+                for _ in range(n_win - own):
+                    self.engine.average(MERGE_RULES[self.merge])
+            except Exception as e:  # libg2v already left the communicator
+                err = e
             finally:
                 # later train() calls of this engine (not data-parallel) merge nothing
                 self.engine.set_option(N.OPT_MERGE_EVERY_JOBS, 0)
-            for _ in range(n_win - own):
-                self.engine.average(MERGE_RULES[self.merge])
+            # RCCL merges are enqueued, not waited for: a rank whose call failed
+            # leaves its peers' merge kernels waiting on the device.  Every rank
+            # learns of a failure here and leaves the communicator too
+            # (ncclCommAbort) instead of hanging in the next collective.
+            if self._min(0 if err is not None else 1) == 0:
+                if err is not None:
+                    raise err
+                self.engine.comm_abort()
+                raise RuntimeError("replica merge aborted: another rank's training call failed")
             self.averages += n_win
             return
         for w in range(n_win):
@@ -269,8 +352,13 @@ class ReplicaTrainer:
             if world > 1:
                 self.sync_replicas()
 
+    def _min(self, v):
+        if self._agree is not None:
+            return int(self._agree(int(v)))
+        return allreduce_min_int(v, self.group)
+
     def sync_replicas(self):
-        if self.backend == "rccl":
+        if self.backend == "libg2v":
             self.engine.average(MERGE_RULES[self.merge])
         elif self.merge == "touch":
             touch_merge_(self.tables, self.olds, self.beta, self.group)

@@ -101,6 +101,30 @@ def count_ids(ids, V):
 # ---------------------------------------------------------------------------
 # device context
 # ---------------------------------------------------------------------------
+class LocalGroup:
+    """g2v_local_group: ``nranks`` replicas of one process on one GPU, each
+    engine driven by its own thread, merging through a device sum in place of
+    ncclAllReduce (the multi-replica merge path on a one-GPU box, where RCCL
+    refuses two ranks).  Destroy it after its engines' last collective."""
+
+    def __init__(self, nranks, timeout_s=0):
+        h = C.c_void_p()
+        N.check(N.lib().g2v_local_group_create(int(nranks), int(timeout_s), C.byref(h)))
+        self._h = h
+        self.nranks = nranks
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().g2v_local_group_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class SGNSEngine:
     """One g2v_ctx on one GPU (one host thread drives it)."""
 
@@ -208,8 +232,8 @@ class SGNSEngine:
         assert len(job_alpha) == n and len(job_seed) == n
         flags = (mode | (N.FLAG_TIMING if timing else 0)
                  | (N.FLAG_COMPUTE_LOSS if compute_loss else 0))
-        N.check(self._lib.g2v_train(self._h, N.ptr(job_sent), N.ptr(job_alpha), N.ptr(job_seed),
-                                    n, flags))
+        self._check_coll(self._lib.g2v_train(self._h, N.ptr(job_sent), N.ptr(job_alpha),
+                                             N.ptr(job_seed), n, flags))
 
     def step_explicit(self, center, inp, negs, alpha, mode=N.MODE_SEQUENTIAL, timing=False,
                       compute_loss=False):
@@ -249,7 +273,7 @@ class SGNSEngine:
         N.check(self._lib.g2v_comm_init(self._h, buf, nranks, rank))
 
     def average(self, rule=N.MERGE_TOUCH):
-        N.check(self._lib.g2v_average(self._h, rule))
+        self._check_coll(self._lib.g2v_average(self._h, rule))
 
     def merge_snapshot(self):
         N.check(self._lib.g2v_merge_snapshot(self._h))
@@ -258,6 +282,37 @@ class SGNSEngine:
     def average_local(engines, rule=N.MERGE_TOUCH):
         arr = (C.c_void_p * len(engines))(*[e._h.value for e in engines])
         N.check(N.lib().g2v_average_local(arr, len(engines), rule))
+
+    def comm_init_local(self, group, rank):
+        """Join an in-process replica group (g2v_comm_init_local; collective:
+        every rank calls it from its own thread)."""
+        N.check(self._lib.g2v_comm_init_local(self._h, group._h, rank))
+        self._group = group
+
+    def comm_init_host(self, collective, nranks, rank):
+        """Merge over a host collective (g2v_comm_init_host).  ``collective(op,
+        buf)`` performs op (N.COLL_SUM / N.COLL_BCAST0) in place on the float32
+        numpy array ``buf`` across the ranks.  An exception inside it fails the
+        libg2v call (G2V_ECOMM) and is re-raised from it."""
+        def tramp(_user, op, buf, count):
+            try:
+                collective(op, np.ctypeslib.as_array(buf, shape=(count,)))
+                return 0
+            except BaseException as e:  # noqa: BLE001 - crosses the C ABI
+                self._coll_error = e
+                return 1
+        self._coll_error = None
+        self._coll_fn = N.COLLECTIVE_FN(tramp)  # kept alive with the engine
+        self._check_coll(self._lib.g2v_comm_init_host(self._h, self._coll_fn, None, nranks, rank))
+
+    def _check_coll(self, rc):
+        err, self._coll_error = getattr(self, "_coll_error", None), None
+        if rc != N.G2V_OK and err is not None:
+            raise err
+        return N.check(rc)
+
+    def comm_abort(self):
+        N.check(self._lib.g2v_comm_abort(self._h))
 
     def sync(self):
         N.check(self._lib.g2v_sync(self._h))

@@ -234,6 +234,11 @@ def main(argv=None):
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
     parser.add_argument("--merge-every-jobs", type=int, default=1024,
                         help="data-parallel replica merge cadence (gensim jobs per rank)")
+    parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
+                        default="auto",
+                        help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
+                             "collective (gloo) = auto; torch = torch-owned tables merged by "
+                             "torch.distributed")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "
@@ -333,6 +338,7 @@ def main(argv=None):
                   device=args.device, mode=args.mode, data_parallel=world > 1)
         import gene2vec_amd.word2vec as W
         W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
+        W.DP_MERGE_TRANSPORT = args.merge_transport
         model = None
         for current_iter in range(1, args.iters + 1):
             name = os.path.join(export_dir, f"gene2vec_dim_{dimension}_iter_{current_iter}")

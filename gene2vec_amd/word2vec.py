@@ -294,6 +294,10 @@ def _load_npz(fname):
 # ---------------------------------------------------------------------------
 # replica merge cadence for data-parallel training (gensim jobs per rank)
 DP_MERGE_EVERY_JOBS = 1024
+# merge transport under torch.distributed: "auto" = libg2v over RCCL for nccl,
+# libg2v over the host collective for gloo; "torch" = torch-owned tables merged
+# by torch.distributed (the CLI's --merge-transport)
+DP_MERGE_TRANSPORT = "auto"
 
 
 def crc32_hash(s):
@@ -455,18 +459,31 @@ class Word2Vec:
         (Python's hash() seeds the init differently in every process) and
         merges the replicas itself every ``merge_every_jobs`` jobs (fused HIP
         kernels + ncclAllReduce over xGMI).  Backend "gloo" (ranks sharing one
-        GPU, which RCCL refuses): torch-owned tables merged by torch.distributed."""
+        GPU, which RCCL refuses): the same libg2v merge with its all-reduce
+        carried by gloo through the host (g2v_comm_init_host); with
+        ``DP_MERGE_TRANSPORT = "torch"``, torch-owned tables merged by
+        torch.distributed."""
         import torch
         import torch.distributed as dist
         mode = N.MODE_SEQUENTIAL if self.mode == "sequential" else N.MODE_HOGWILD
         rank, world = dist.get_rank(), dist.get_world_size()
-        if dist.get_backend() == "nccl":
+        transport = DP_MERGE_TRANSPORT
+        if transport == "auto":
+            transport = "rccl" if dist.get_backend() == "nccl" else "host"
+        if transport == "rccl":
             box = [eng.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(box, src=0)
             eng.comm_init(box[0], world, rank)
             self._replica = Dd.ReplicaTrainer(eng, (), self.merge_every_jobs, mode,
-                                              backend="rccl")
+                                              backend="libg2v")
             return
+        if transport == "host":
+            eng.comm_init_host(Dd.host_collective(), world, rank)
+            self._replica = Dd.ReplicaTrainer(eng, (), self.merge_every_jobs, mode,
+                                              backend="libg2v")
+            return
+        if transport != "torch":
+            raise ValueError(f"merge transport {transport!r}")
         dev = torch.device("cuda", self.device)
         # engine launches, merges and collectives ordered on one non-default stream
         stream = torch.cuda.Stream(dev)

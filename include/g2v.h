@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define G2V_ABI_VERSION 2
+#define G2V_ABI_VERSION 3
 
 /* status codes */
 #define G2V_OK 0
@@ -83,6 +83,11 @@ typedef struct g2v_stats {
      * HOGWILD/MINIBATCH launches add per-wave float32 partial sums in double
      * (gensim's own workers>1 tally is a racy read-modify-write of that float). */
     double training_loss;
+    /* layout of the last Hogwild SGNS launch (ABI 3): workgroups, hot-row
+     * stripes (rows x copies) and the second tier (rows below stripe2_rows x
+     * copies); the defaults are derived from the vocabulary at g2v_set_vocab */
+    int64_t sgns_grid;
+    int64_t stripe_rows, stripe_copies, stripe2_rows, stripe2_copies;
 } g2v_stats;
 
 /* ---- errors / version --------------------------------------------------- */
@@ -109,7 +114,9 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         stores [1]
  *   G2V_OPT_SEG_JOBS      gensim jobs per sampling/update segment [1024]
  *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = the staleness-bounded
- *                         default (g2v_get_option reads it) [0]
+ *                         default, RECOMPUTED by every g2v_set_vocab from the
+ *                         vocabulary (g2v_get_option reads the value in use;
+ *                         g2v_stats reports the last launch's) [0]
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
  *                         2 uncached (re-allocates, zero-filled) [0]
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
@@ -140,7 +147,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         call's last, shorter one -- with the replica merge
  *                         of g2v_average, on the same stream; every rank must
  *                         make the same number of merges (0 = off) [0]
- *   G2V_OPT_MERGE_RULE    rule of those merges, G2V_MERGE_TOUCH / _MEAN [TOUCH] */
+ *   G2V_OPT_MERGE_RULE    rule of those merges, G2V_MERGE_TOUCH / _MEAN [TOUCH]
+ *   G2V_OPT_ACTIVE_WAVES  Hogwild kernel: waves per workgroup that train, 1..4;
+ *                         with G2V_OPT_GRID 1 and 1 wave the production kernel
+ *                         runs its chunks in record order, a deterministic
+ *                         update order (parity checks) [4] */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
@@ -155,6 +166,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_MERGE_RULE 12
 #define G2V_OPT_STRIPE2_ROWS 13
 #define G2V_OPT_STRIPE2_COPIES 14
+#define G2V_OPT_ACTIVE_WAVES 15
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest
@@ -177,7 +189,8 @@ int g2v_set_vocab(g2v_ctx *ctx, const int64_t *counts, double sample, double ns_
 /* ---- weights --------------------------------------------------------------- */
 /* Borrow device tables (e.g. torch-owned, so torch.distributed can all-reduce
  * them): syn0 = [ext] wv.vectors, syn1neg = [ext] trainables.syn1neg, both
- * [V][ld] fp32, ld >= g2v_row_stride and a multiple of 4.  NULL, NULL returns
+ * [V][ld] fp32, ld >= D and a multiple of 4, each table below 2 GiB (the
+ * kernels' 32-bit buffer offsets; G2V_ERANGE otherwise).  NULL, NULL returns
  * to context-owned tables. */
 int g2v_bind_tables(g2v_ctx *ctx, float *syn0_dev, float *syn1neg_dev, int64_t ld);
 /* Upload host [V][D] tables (+ optional vectors_lockf[V], NULL = ones).
@@ -281,6 +294,45 @@ int g2v_merge_snapshot(g2v_ctx *ctx);
  * trained by separate contexts, e.g. one per stream): no RCCL, one kernel.
  * Every context needs a snapshot (g2v_merge_snapshot) and equal V, D, ld. */
 int g2v_average_local(g2v_ctx *const *ctxs, int n, int merge_rule);
+
+/* Two more transports for the merge of g2v_average / G2V_OPT_MERGE_EVERY_JOBS.
+ * Only the all-reduce (and the initial broadcast) changes; the delta and apply
+ * kernels, the touch/mean rules and the in-call merges of g2v_train are the
+ * RCCL path's own, so every merge line that runs under RCCL also runs here.
+ *
+ * In-process group: nranks contexts of one process on one device, each driven
+ * by its own host thread (calls into different contexts may run concurrently).
+ * The all-reduce is a device sum of the ranks' buffers in rank order (the order
+ * of g2v_average_local, whose results it reproduces bit for bit), ordered by
+ * HIP events, the ranks meeting at a host barrier.  A rank that fails inside a
+ * collective aborts the group: the others return G2V_ECOMM instead of waiting
+ * (also after timeout_s seconds at a barrier, 0 = 600).  The group must
+ * outlive its contexts' collectives; destroy it after them. */
+typedef struct g2v_local_group g2v_local_group;
+int g2v_local_group_create(int nranks, int timeout_s, g2v_local_group **out);
+int g2v_local_group_destroy(g2v_local_group *group);
+/* Collective over the group's ranks (each calls it once, from its own thread):
+ * rank 0's tables are copied to every rank, which records them as its merge
+ * snapshot (as g2v_comm_init does). */
+int g2v_comm_init_local(g2v_ctx *ctx, g2v_local_group *group, int rank);
+
+/* Host transport: fn performs the collective on host memory, in place, over
+ * whatever carries the ranks' traffic (e.g. torch.distributed gloo); it is
+ * called on the thread of the g2v call, after the device buffers were copied to
+ * pinned host memory, and must return 0 (anything else: G2V_ECOMM).
+ *   G2V_COLL_SUM    buf[count] <- the sum over ranks of every rank's buf
+ *   G2V_COLL_BCAST0 buf[count] <- rank 0's buf */
+#define G2V_COLL_SUM 0
+#define G2V_COLL_BCAST0 1
+typedef int (*g2v_collective_fn)(void *user, int op, float *buf, int64_t count);
+int g2v_comm_init_host(g2v_ctx *ctx, g2v_collective_fn fn, void *user, int nranks, int rank);
+
+/* Leave the communicator after a failure: RCCL's ncclCommAbort (in-flight
+ * collectives of this rank are torn down instead of waiting for peers that
+ * will never arrive), the in-process group's abort (its other ranks return
+ * G2V_ECOMM).  g2v_train calls it itself when it fails between in-call merges.
+ * The context stays usable without a communicator. */
+int g2v_comm_abort(g2v_ctx *ctx);
 
 /* ---- text exporters ------------------------------------------------------------- */
 /* Row text of the two exporters, every float32 printed as numpy's

@@ -165,3 +165,22 @@ def count_records(tok, sent_off, job_sent, job_seed, sample_int, sample_on, cum,
                                     C.c_int64(len(job_sent) - 1), _p(job_seed), _p(si),
                                     C.c_int(int(bool(sample_on))), _p(cum), C.c_int32(len(cum)),
                                     C.c_int32(K), None, C.c_int64(0)))
+
+
+def atomic_one_wave(syn0, syn1neg, lockf, center, inp, negs, alpha, stripe_rows=0,
+                    stripe_copies=1, stripe2_rows=0, stripe2_copies=1, chunk=32):
+    """k_sgns_atomic's update order on one wave (orc_atomic_one_wave): in place
+    on [V][D] float32 tables.  stripe_* describe the hot-row copies the kernel
+    used (g2v_stats.stripe_*)."""
+    V, D = syn0.shape
+    center = np.ascontiguousarray(center, dtype=np.int32)
+    inp = np.ascontiguousarray(inp, dtype=np.int32)
+    negs = np.ascontiguousarray(negs, dtype=np.int32)
+    lockf = np.ascontiguousarray(lockf, dtype=np.float32)
+    assert syn0.dtype == np.float32 and syn0.flags.c_contiguous
+    assert syn1neg.dtype == np.float32 and syn1neg.flags.c_contiguous
+    lib().orc_atomic_one_wave(_p(syn0), _p(syn1neg), _p(lockf), C.c_int64(D), C.c_int32(D),
+                              C.c_int32(negs.shape[1]), _p(center), _p(inp), _p(negs),
+                              C.c_int64(len(center)), C.c_float(alpha), C.c_int32(stripe_rows),
+                              C.c_int32(stripe_copies), C.c_int32(stripe2_rows),
+                              C.c_int32(stripe2_copies), C.c_int32(chunk))

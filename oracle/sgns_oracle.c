@@ -319,3 +319,194 @@ void orc_sgns_step_sequential(float *syn0, float *syn1neg, const float *lockf, i
                negs + e * K, loss, NULL);
     free(work);
 }
+
+/* ---------------------------------------------------------------------------
+ * orc_atomic_one_wave: the update ORDER of the production Hogwild kernel
+ * (gene2vec_amd/csrc/g2v_sgns_atomic.hip, k_sgns_atomic) run on one wave
+ * (G2V_OPT_GRID 1, G2V_OPT_ACTIVE_WAVES 1), restated so its arithmetic on
+ * REPEATED rows can be checked (the disjoint-row checks cannot see it).  The
+ * per-example math is fast_sentence_sg_neg's (A.5, sg_neg above); what
+ * differs from gensim's sequential order, as the kernel documents it:
+ *   - chunks of `chunk` consecutive examples; inside a chunk, example e+1's
+ *     rows are read after e-1's deltas landed and BEFORE e's (the wave issues
+ *     e's atomics behind e+1's loads); a chunk's first example sees everything
+ *     before it;
+ *   - all K+1 dots of an example are taken from the rows as loaded; a target
+ *     repeated within the example takes the earlier copy's updated row and, if
+ *     that one was updated, recomputes its dot (gensim's own semantics);
+ *   - every delta is coef * src (float) added to the row in memory (a float
+ *     atomic): syn1neg[t] += g * l1 per applied target, then syn0[input] +=
+ *     lockf * work;
+ *   - hot-row stripes: rows [0, R1) of each table have C1-1 extra copies,
+ *     rows [R1, R2) C2-1 (C2 a power of two); a read is main + copies summed in
+ *     copy order; the delta of target d (d = K+1 for syn0) goes to copy
+ *     (cbase + d) mod C1 (tier 1) or (cbase + d) & (C2-1) (tier 2), copy 0 =
+ *     the main row, cbase = e mod C1; after the launch every copy is folded
+ *     into its main row in copy order and zeroed.
+ * The tables are [V][ld] (ld >= D), updated in place.
+ * ------------------------------------------------------------------------- */
+typedef struct {
+    float *dst;
+    float coef;
+    int src; /* 0 = l1, 1 = work */
+} orc_op;
+
+static float *orc_row(float *main, float *cp1, float *cp2, int64_t ld, int D, int tbl, int32_t t,
+                      int c, int R1, int C1, int R2, int C2) {
+    /* row t of table tbl, copy c (0 = main) */
+    if (c == 0) return main + (int64_t)t * ld;
+    if (t < R1) return cp1 + (((int64_t)tbl * R1 + t) * (C1 - 1) + (c - 1)) * D;
+    return cp2 + (((int64_t)tbl * (R2 - R1) + (t - R1)) * (C2 - 1) + (c - 1)) * D;
+}
+
+static void orc_read_row(float *out, float *main, float *cp1, float *cp2, int64_t ld, int D,
+                         int tbl, int32_t t, int R1, int C1, int R2, int C2) {
+    memcpy(out, main + (int64_t)t * ld, sizeof(float) * D);
+    int C = t < R1 ? C1 : (t < R2 ? C2 : 1);
+    for (int c = 1; c < C; c++) {
+        const float *p = orc_row(main, cp1, cp2, ld, D, tbl, t, c, R1, C1, R2, C2);
+        for (int i = 0; i < D; i++) out[i] = out[i] + p[i];
+    }
+}
+
+void orc_atomic_one_wave(float *syn0, float *syn1neg, const float *lockf, int64_t ld, int32_t D,
+                         int32_t K, const int32_t *center, const int32_t *input,
+                         const int32_t *negs, int64_t n, float alpha, int32_t R1, int32_t C1,
+                         int32_t R2, int32_t C2, int32_t chunk) {
+    ensure_exp();
+    if (C1 < 1) C1 = 1;
+    if (C2 < 1 || R2 <= R1) { C2 = 1; R2 = R1; }
+    if (C1 == 1) { R1 = 0; R2 = 0; C2 = 1; }
+    const int NT = K + 1;
+    float *cp1 = (float *)calloc((size_t)2 * (R1 ? R1 : 1) * C1 * D, sizeof(float));
+    float *cp2 = (float *)calloc((size_t)2 * (R2 - R1 + 1) * C2 * D, sizeof(float));
+    float *l1 = (float *)malloc(sizeof(float) * D);
+    float *rw = (float *)malloc(sizeof(float) * D * NT);
+    float *work = (float *)malloc(sizeof(float) * D);
+    /* the deltas still in flight: example e-1's (sources copied) */
+    float *p_l1 = (float *)malloc(sizeof(float) * D);
+    float *p_work = (float *)malloc(sizeof(float) * D);
+    orc_op *pend = (orc_op *)malloc(sizeof(orc_op) * (NT + 1));
+    int npend = 0;
+    int32_t tg[64];
+    float *tab[2] = {syn0, syn1neg};
+
+#define ORC_APPLY()                                                             \
+    do {                                                                        \
+        for (int o_ = 0; o_ < npend; o_++) {                                    \
+            const float *s_ = pend[o_].src ? p_work : p_l1;                     \
+            for (int i_ = 0; i_ < D; i_++) {                                    \
+                const float v_ = pend[o_].coef * s_[i_];                        \
+                pend[o_].dst[i_] = pend[o_].dst[i_] + v_;                       \
+            }                                                                   \
+        }                                                                       \
+        npend = 0;                                                              \
+    } while (0)
+
+#define ORC_LOAD(e_)                                                                    \
+    do {                                                                                \
+        tg[0] = center[e_];                                                             \
+        for (int d_ = 0; d_ < K; d_++) tg[d_ + 1] = negs[(e_) * K + d_];                \
+        orc_read_row(l1, syn0, cp1, cp2, ld, D, 0, input[e_], R1, C1, R2, C2);           \
+        for (int d_ = 0; d_ <= K; d_++) {                                               \
+            if (tg[d_] >= 0)                                                            \
+                orc_read_row(rw + (int64_t)d_ * D, syn1neg, cp1, cp2, ld, D, 1, tg[d_], R1, \
+                             C1, R2, C2);                                               \
+            else                                                                        \
+                memset(rw + (int64_t)d_ * D, 0, sizeof(float) * D);                     \
+        }                                                                               \
+    } while (0)
+
+    for (int64_t cs = 0; cs < n; cs += chunk) {
+        const int64_t ce = cs + chunk < n ? cs + chunk : n;
+        ORC_APPLY();
+        ORC_LOAD(cs);
+        int cbase = (int)(cs % C1);
+        for (int64_t e = cs; e < ce; e++) {
+            float fv[64], lv[64], g[64];
+            int live[64], dirty[64];
+            for (int d = 0; d <= K; d++) {
+                fv[d] = tg[d] >= 0 ? dsdot(l1, rw + (int64_t)d * D, D) : 0.0f;
+                const int in = fv[d] > -(float)MAX_EXP && fv[d] < (float)MAX_EXP;
+                lv[d] = g_exp_table[in ? (int)((fv[d] + MAX_EXP) * LUT_SCALE) : 0];
+            }
+            memset(work, 0, sizeof(float) * D);
+            int any = 0;
+            for (int d = 0; d <= K; d++) {
+                g[d] = 0.0f;
+                live[d] = 0;
+                dirty[d] = 0;
+                if (tg[d] < 0) continue;
+                int prev_dirty = 0;
+                for (int d2 = 0; d2 < d; d2++)
+                    if (tg[d2] == tg[d]) {
+                        memcpy(rw + (int64_t)d * D, rw + (int64_t)d2 * D, sizeof(float) * D);
+                        prev_dirty = dirty[d2];
+                    }
+                float f = fv[d], lut = lv[d];
+                if (prev_dirty) {
+                    f = dsdot(l1, rw + (int64_t)d * D, D);
+                    dirty[d] = 1;
+                    if (f > -(float)MAX_EXP && f < (float)MAX_EXP)
+                        lut = g_exp_table[(int)((f + MAX_EXP) * LUT_SCALE)];
+                }
+                if (f <= -(float)MAX_EXP || f >= (float)MAX_EXP) continue;
+                const float gg = ((d == 0 ? 1.0f : 0.0f) - lut) * alpha;
+                float *r = rw + (int64_t)d * D;
+                for (int i = 0; i < D; i++) {
+                    work[i] = fmaf(gg, r[i], work[i]);
+                    r[i] = fmaf(gg, l1[i], r[i]);
+                }
+                g[d] = gg;
+                live[d] = 1;
+                dirty[d] = 1;
+                any = 1;
+            }
+            /* e-1's deltas land, e+1's rows are read, then e's deltas issue */
+            ORC_APPLY();
+            memcpy(p_l1, l1, sizeof(float) * D);
+            memcpy(p_work, work, sizeof(float) * D);
+            const int32_t in_e = input[e];
+            int32_t tg_e[64];
+            memcpy(tg_e, tg, sizeof(int32_t) * NT);
+            if (e + 1 < ce) ORC_LOAD(e + 1);
+            for (int d = 0; d <= NT; d++) {
+                const int w = d == NT;
+                if (w ? !any : !live[d]) continue;
+                const int32_t t = w ? in_e : tg_e[d];
+                const int craw = cbase + d;
+                int c;
+                if (t >= R1 && t < R2) c = craw & (C2 - 1);
+                else if (t < R1) c = craw % C1;
+                else c = 0;
+                pend[npend].dst = orc_row(tab[w ? 0 : 1], cp1, cp2, ld, D, w ? 0 : 1, t, c, R1, C1,
+                                          R2, C2);
+                pend[npend].coef = w ? (lockf ? lockf[t] : 1.0f) : g[d];
+                pend[npend].src = w;
+                npend++;
+            }
+            cbase = cbase + 1 == C1 ? 0 : cbase + 1;
+        }
+    }
+    ORC_APPLY();
+    /* k_fold_stripes: main += copies in copy order, copies = 0 */
+    for (int tbl = 0; tbl < 2; tbl++)
+        for (int32_t t = 0; t < R2; t++) {
+            const int C = t < R1 ? C1 : C2;
+            float *m = tab[tbl] + (int64_t)t * ld;
+            for (int c = 1; c < C; c++) {
+                const float *p = orc_row(tab[tbl], cp1, cp2, ld, D, tbl, t, c, R1, C1, R2, C2);
+                for (int i = 0; i < D; i++) m[i] = m[i] + p[i];
+            }
+        }
+#undef ORC_APPLY
+#undef ORC_LOAD
+    free(cp1);
+    free(cp2);
+    free(l1);
+    free(rw);
+    free(work);
+    free(p_l1);
+    free(p_work);
+    free(pend);
+}

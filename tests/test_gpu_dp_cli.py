@@ -1,9 +1,11 @@
 """GPU: data-parallel CLI -- `torchrun --nproc-per-node N -m gene2vec_amd.gene2vec
 data out txt` trains one replica per rank on a contiguous shard of the shuffled
-pairs and merges the replicas row-wise over the process group (the
-reference itself is one process, src/gene2vec.py:59).  The round's box has one
-GPU, so two ranks share cuda:0 over gloo here; the 8-GPU node runs the same code
-over RCCL.  Checks: rank 0 alone writes the outputs every rank reloads, and the
+pairs and merges the replicas row-wise (the reference itself is
+one process, src/gene2vec.py:59).  The round's box has one GPU, so two ranks
+share cuda:0 over gloo here: the merge is libg2v's own (delta/apply kernels,
+in-call merges, rank-0 broadcast), its all-reduce carried by gloo through the
+host (--merge-transport host, the gloo default); the 8-GPU node runs the same
+merge over RCCL.  One test keeps the torch-tensor merge (--merge-transport torch).  Checks: rank 0 alone writes the outputs every rank reloads, and the
 model's held-in SGNS objective improves at least 93 % as much as the
 single-process run's (measured 97 %)."""
 import os
@@ -64,7 +66,7 @@ def test_cli_data_parallel_two_ranks(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
-           "--backend", "gloo"] + opts
+           "--backend", "gloo", "--merge-transport", "host"] + opts
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
@@ -135,7 +137,8 @@ def test_cli_data_parallel_ragged_corpus_falls_back(tmp_path):
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
            "--backend", "gloo", "--iters", "2", "--dim", "16", "--hash", "crc32",
-           "--shuffle-seed", "2", "--native-ingest", "--no-txt", "--no-w2v"]
+           "--shuffle-seed", "2", "--native-ingest", "--no-txt", "--no-w2v",
+           "--merge-transport", "torch"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     assert "using Python's shuffle" in r.stdout

@@ -27,7 +27,7 @@ def test_library_loads_and_exports_header():
         assert hasattr(L, s), s
         assert s in N.SIGNATURES, f"{s} missing from the ctypes signature table"
     assert set(N.SIGNATURES) == set(syms)
-    assert L.g2v_abi_version() == N.ABI_VERSION == 2
+    assert L.g2v_abi_version() == N.ABI_VERSION == 3
 
 
 def test_error_path_without_gpu_is_loud():
@@ -44,6 +44,37 @@ def test_error_path_without_gpu_is_loud():
     assert rc == N.G2V_EINVAL
     rc = N.lib().g2v_create(0, 3_000_000, 200, 5, 1, C.byref(h))  # > 2 GiB per table
     assert rc == N.G2V_EINVAL and b"2 GiB" in N.lib().g2v_last_error()
+
+
+def test_local_group_arguments_without_gpu():
+    """g2v_local_group_create / _destroy are host-only: argument checks and a
+    create/destroy round trip need no device"""
+    import ctypes as C
+    L = N.lib()
+    h = C.c_void_p()
+    assert L.g2v_local_group_create(0, 0, C.byref(h)) == N.G2V_EINVAL
+    assert L.g2v_local_group_create(17, 0, C.byref(h)) == N.G2V_EINVAL  # > kMaxLocalReplicas
+    assert L.g2v_local_group_create(2, -1, C.byref(h)) == N.G2V_EINVAL
+    assert L.g2v_local_group_create(4, 0, C.byref(h)) == N.G2V_OK and h.value
+    assert L.g2v_local_group_destroy(h) == N.G2V_OK
+    assert L.g2v_local_group_destroy(None) == N.G2V_OK
+    # a context is required for the collectives themselves
+    assert L.g2v_comm_init_local(None, None, 0) == N.G2V_EINVAL
+    assert L.g2v_comm_abort(None) == N.G2V_EINVAL
+
+
+def test_stats_struct_matches_header():
+    """g2v_stats as the header declares it: the ctypes mirror has the same
+    fields in the same order (ABI 3 appended the launch layout)"""
+    src = open(os.path.join(ROOT, "include", "g2v.h")).read()
+    body = re.search(r"typedef struct g2v_stats \{(.*?)\} g2v_stats;", src, re.S).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = []
+    for decl in body.split(";"):
+        decl = decl.strip()
+        if decl:
+            names += [x.strip() for x in decl.split(None, 1)[1].split(",")]
+    assert names == [f for f, _ in N.Stats._fields_]
 
 
 @pytest.mark.parametrize("lengths", [[2] * 40, [2] * 12345, [2, 4, 0, 2, 3, 9997, 2, 10000, 1] * 3,

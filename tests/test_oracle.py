@@ -227,3 +227,34 @@ def test_long_sentence_truncation_numpy_equals_c(sample):
         effs.append(O.downsample_job(sents[s0:s1], si, int(sd), sample != 0)[2])
     assert rec.tolist() == [[c, j] + n for c, j, n in ref]
     assert max(effs) == 10000 and effs[0] == 0
+
+
+def test_atomic_one_wave_restatement_degenerates_to_sequential():
+    """orc_atomic_one_wave (k_sgns_atomic's order on one wave) with chunks of
+    one example and no stripes is gensim's sequential order, up to the
+    kernel's float atomics rounding coef*src and the add separately where
+    saxpy fuses them (~1e-7); with 32-example chunks the one-example lag
+    moves it by ~0.5 %, and stripes only re-associate sums (~1e-6)"""
+    from oracle import c_oracle as CO
+    rng = np.random.RandomState(0)
+    V, D, K, n = 40, 200, 5, 3000
+    s0 = ((rng.rand(V, D) - 0.5) / D).astype(np.float32)
+    s1 = np.zeros((V, D), np.float32)
+    c, i = rng.randint(0, V, n), rng.randint(0, V, n)
+    ng = rng.randint(0, V, (n, K))
+    ng[ng == c[:, None]] = -1
+    lf = np.ones(V, np.float32)
+
+    def rel(a, b):
+        return float(np.abs(a - b).max() / np.abs(b).max())
+    a0, a1 = s0.copy(), s1.copy()
+    CO.sgns_step_sequential(a0, a1, lf, c, i, ng, 0.025)
+    b0, b1 = s0.copy(), s1.copy()
+    CO.atomic_one_wave(b0, b1, lf, c, i, ng, 0.025, chunk=1)
+    assert rel(b0, a0) < 1e-6 and rel(b1, a1) < 1e-6
+    d0, d1 = s0.copy(), s1.copy()
+    CO.atomic_one_wave(d0, d1, lf, c, i, ng, 0.025, chunk=32)
+    assert rel(d1, a1) > 1e-3
+    f0, f1 = s0.copy(), s1.copy()
+    CO.atomic_one_wave(f0, f1, lf, c, i, ng, 0.025, 8, 16, 20, 4, chunk=32)
+    assert rel(f0, d0) < 1e-5 and rel(f1, d1) < 1e-5
