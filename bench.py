@@ -100,9 +100,12 @@ def parse():
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                         "the N>1 path with several ranks sharing one GPU)")
+    p.add_argument("--merge-transport", choices=("auto", "torch"), default="auto",
+                   help="N>1: auto = libg2v's merge over RCCL (nccl) or over the host "
+                        "collective (gloo); torch = torch.distributed merges the bound tables")
     p.add_argument("--traffic-json", default=None,
                    help="PMC bytes per example for roofline.traffic (default: the newest "
-                        "profiles/traffic_r*.json whose workload matches)")
+                        "profiles/**/traffic_r*.json of this workload measured on this kernel build)")
     return p.parse_args()
 
 
@@ -198,7 +201,7 @@ def main():
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
     merge_backend = "torch"
     merge_note = None
-    if use_dist and a.backend == "nccl":
+    if use_dist and a.backend == "nccl" and a.merge_transport == "auto":
         # libg2v's own RCCL communicator: rank 0's unique id over the process group
         box = [eng.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
@@ -211,8 +214,12 @@ def main():
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if ok.item() == 0:  # every rank must merge the same way
             merge_backend = "torch"
+    elif use_dist and a.merge_transport == "auto":
+        # gloo rehearsal: libg2v's merge, its all-reduce carried through the host
+        eng.comm_init_host(Dd.host_collective(), world, rank)
+        merge_backend = "libg2v-host"
     trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=a.merge,
-                                backend=merge_backend)
+                                backend="torch" if merge_backend == "torch" else "libg2v")
     torch.cuda.synchronize(dev)
 
     def step(i, timing):
@@ -265,26 +272,39 @@ def main():
     achieved = alg_bytes_launch / (avg_launch_ms / 1e3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic = None
     traffic_src = None
-    # the newest profile of this workload (traffic_<round tag>[_<config>].json)
+    # PMC bytes per example of the same workload (vocabulary, shape,
+    # downsampling and skew) from a separate rocprofv3 --pmc pass of THIS
+    # kernel build (scripts/profile_round.sh -> profiles/traffic_*.json,
+    # stamped with the hash of the kernel's sources), scaled to this run's
+    # examples per launch; a profile of another build is refused (traffic null)
+    from gene2vec_amd.build import kernel_source_hash
+    ksha = kernel_source_hash()
     cands = [a.traffic_json] if a.traffic_json else sorted(
-        glob.glob(os.path.join(ROOT, "profiles", "traffic_r*.json")), reverse=True)
+        glob.glob(os.path.join(ROOT, "profiles", "**", "traffic_r*.json"), recursive=True),
+        reverse=True)
+    stale = []
     for tpath in cands:
         if traffic is not None or not os.path.exists(tpath):
             continue
         try:
             tj = json.load(open(tpath))
-            # per-example PMC bytes of the same workload (vocabulary, shape, downsampling
-            # and skew) from a separate rocprofv3 --pmc pass of this kernel, scaled to
-            # this run's examples per launch
-            if (tj.get("vocab"), tj.get("dim"), tj.get("negative"), tj.get("sample"),
-                    tj.get("zipf")) == (V0, D, K, a.sample, a.zipf):
-                traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
-                                * st["examples"] / launches, 1)
-                traffic_src = (f"{os.path.relpath(tpath, ROOT)}: PMC bytes per "
-                               f"example x this run's {st['examples'] // launches} examples "
-                               "per launch (not measured in this process)")
-        except Exception:
-            traffic = None
+        except (OSError, ValueError):
+            continue
+        if (tj.get("vocab"), tj.get("dim"), tj.get("negative"), tj.get("sample"),
+                tj.get("zipf")) != (V0, D, K, a.sample, a.zipf):
+            continue
+        if tj.get("kernel_src_sha16") != ksha:
+            stale.append(os.path.relpath(tpath, ROOT))
+            continue
+        traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
+                        * st["examples"] / launches, 1)
+        traffic_src = (f"{os.path.relpath(tpath, ROOT)} (kernel build {ksha}): PMC bytes "
+                       f"per example x this run's {st['examples'] // launches} examples per "
+                       "launch (not measured in this process)")
+    if traffic is None:
+        traffic_src = (f"no PMC profile of kernel build {ksha} for this workload"
+                       + (f"; refused profiles of other builds: {', '.join(stale[:3])}"
+                          if stale else ""))
     atomic_bytes = (K + 2) * D * 4  # every SGNS update is a memory-side f32 atomic delta
     atomic_gbps = atomic_bytes * st["examples"] / (st["sgns_kernel_ms"] / 1e3) / 1e9 \
         if st["sgns_kernel_ms"] > 0 else 0.0
@@ -297,6 +317,7 @@ def main():
                                     "of added bytes chip-wide)",
                 "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
                 "atomic_frac": round(atomic_gbps / 1300.0, 4), "traffic_source": traffic_src,
+                "kernel_src_sha16": ksha,
                 "grid_workgroups": eng.get_option(N.OPT_GRID),
                 "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}",
                 "stripes_tier2": f"rows < {eng.get_option(N.OPT_STRIPE2_ROWS)} "
@@ -398,11 +419,13 @@ def main():
                              f"{world}, dim {D}, neg {K}, replica merge ({a.merge}) every "
                              f"{avg_every} jobs: "
                              + ("libg2v g2v_average (RCCL over xGMI)" if merge_backend == "rccl"
+                                else "libg2v merge over gloo (host collective) rehearsal, ranks "
+                                     "sharing a GPU" if merge_backend == "libg2v-host"
                                 else "torch.distributed gloo rehearsal, ranks sharing a GPU"
                                 if a.backend == "gloo" else
                                 "torch.distributed merge (libg2v communicator unavailable)")),
-                "vocab": V, "pairs_per_gpu": n_pairs, "dim": D, "negative": K,
-                "sample": a.sample, "window": 1,
+                "vocab": V, "vocab_requested": V0, "zipf": a.zipf, "pairs_per_gpu": n_pairs,
+                "dim": D, "negative": K, "sample": a.sample, "window": 1,
                 "parallelism": f"dp{world}" + (f" + {merge_backend} {a.merge} merge"
                                                if world > 1 else "")},
             "examples_per_s": round(total_examples / elapsed, 1),

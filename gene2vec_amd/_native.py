@@ -160,7 +160,7 @@ def lib():
     # on it (measured on MI355X: libg2v first -> torch.cuda init fails).
     # `import torch` itself, not just a dlopen of torch's libamdhip64: with the
     # dlopen alone the CLI's 10 training iterations took 19.4 s instead of
-    # 7.3 s on MI355X (profiles/r01_experiments/e2e_runtime_*.json), for the 1.5 s import.
+    # 7.3 s on MI355X (profiles/r01/r01_experiments/e2e_runtime_*.json), for the 1.5 s import.
     try:
         import torch  # noqa: F401
     except ImportError:  # pragma: no cover - torch is plumbing, not required

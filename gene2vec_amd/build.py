@@ -26,6 +26,21 @@ SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(CSRC, "g2v_device.h"),
            os.path.join(ROOT, "include", "g2v.h")]
 ARCH = "gfx950"
+# the sources that determine k_sgns_atomic's code and launch (bench.py accepts a
+# PMC traffic profile only when it was measured on this exact kernel build)
+KERNEL_SOURCES = [os.path.join(CSRC, s) for s in
+                  ("g2v_sgns_atomic.hip", "g2v_device.h", "g2v_internal.h", "g2v_api.hip")]
+
+
+def kernel_source_hash() -> str:
+    """sha256 (first 16 hex digits) of KERNEL_SOURCES, in that order"""
+    import hashlib
+    h = hashlib.sha256()
+    for p in KERNEL_SOURCES:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
 
 
 def hipcc() -> str:

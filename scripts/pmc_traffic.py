@@ -9,6 +9,9 @@ import json
 import os
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
 KERNEL = "k_sgns_atomic"
 
 
@@ -45,9 +48,12 @@ def main(out):
     hit, miss = c.get("TCC_HIT_sum", 0.0), c.get("TCC_MISS_sum", 0.0)
     bpe = b["roofline"]["bytes_per_example"]
     cfg = b["config"]
+    from gene2vec_amd.build import kernel_source_hash
     res = {
-        "vocab": cfg["vocab"], "dim": cfg["dim"], "negative": cfg["negative"],
-        "sample": cfg["sample"], "zipf": 1.0, "kernel": KERNEL,
+        # the kernel build these counters belong to (bench.py refuses any other)
+        "kernel_src_sha16": kernel_source_hash(),
+        "vocab": cfg.get("vocab_requested", cfg["vocab"]), "dim": cfg["dim"], "negative": cfg["negative"],
+        "sample": cfg["sample"], "zipf": cfg.get("zipf", 1.0), "kernel": KERNEL,
         "method": "rocprofv3 --pmc, one counter group per run (scripts/profile_round.sh), "
                   "10 M-pair bench; FETCH_SIZE x2 (gfx950 16-B/lane read correction), "
                   "WRITE_SIZE as is (KB units); summed over the SGNS launches / examples",

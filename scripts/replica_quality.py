@@ -1,0 +1,275 @@
+"""Data-parallel quality at the configuration C3 runs (verdict r2 item 1).
+
+The reference trains ONE model with 32 Hogwild threads (src/gene2vec.py:59,70);
+C3 trains 8 replicas on 8 x 125 M pairs and merges them with libg2v's touch
+rule every --merge-every jobs.  This script runs both on ONE GPU and compares
+them on the same corpus, the same per-iteration shuffles and the reference's
+10-iteration alpha sawtooth (src/gene2vec.py:67-92):
+
+  replicas  R engines, one host thread each, an in-process replica group
+            (g2v_comm_init_local: libg2v's delta/apply kernels and in-call
+            merges, the all-reduce a device sum) -- the production merge path
+            of the data-parallel CLI (word2vec.Word2Vec._bind_replica /
+            distributed.ReplicaTrainer), rank r training the r-th contiguous
+            1/R of each iteration's permutation with its own job seeds and its
+            shard's alpha schedule (word2vec.Word2Vec.train_ids)
+  single    one engine over the whole permutation (gensim's one model)
+
+Corpus ("C3q"): C3's synthetic Zipf(1) pairs over 24,447 genes (R shards of
+bench.py's generator) plus the positive pairs of the reference's GGIPNN splits
+(data/predictionData, all three) repeated --ggipnn-repeat times, so the run
+also carries real gene-pair structure: a label-leaky harness (test positives
+are trained on) that measures data-parallel vs single-model parity only, as
+scripts/ggipnn_e2e.py does.  Metrics after the last iteration:
+  heldin   SGNS objective on 50,000 corpus pairs (K unigram^0.75 negatives)
+  auc      GGIPNN test AUC (gene2vec_amd/ggipnn.py) on the exported .txt,
+           mean over --auc-seeds classifier seeds
+  target   the manuscript target function (gene2vec_amd/evaluate.py) on a
+           synthetic .gmt: neighbourhoods of the positive-pair graph
+           (MSigDB is absent)
+
+    python scripts/replica_quality.py --merge-every 1024,4096 --out gpurun_out/rq
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from gene2vec_amd import _native as N  # noqa: E402
+from gene2vec_amd import distributed as Dd  # noqa: E402
+from gene2vec_amd import engine as E  # noqa: E402
+from gene2vec_amd import synthetic as S  # noqa: E402
+
+DATA = os.path.join(ROOT, "data", "predictionData")
+
+
+def positives():
+    out = []
+    for part in ("train", "valid", "test"):
+        text = open(os.path.join(DATA, f"{part}_text.txt")).read().splitlines()
+        lab = open(os.path.join(DATA, f"{part}_label.txt")).read().splitlines()
+        out += [t.split() for t, l in zip(text, lab) if l == "1" and len(t.split()) == 2]
+    return out
+
+
+def build_corpus(R, per, V0, rep, seed):
+    """(pairs int32[N][2] in id space, names by id, positive pairs by name)"""
+    with ThreadPoolExecutor(max_workers=min(R, 16)) as ex:
+        shards = list(ex.map(lambda r: S.zipf_gene_pairs(per, V0, 1.0, seed=20250114, shard=r),
+                             range(R)))
+    names = S.gene_names(V0)
+    pos = positives()
+    gid = {}
+    for a, b in pos:
+        for g in (a, b):
+            if g not in gid:
+                gid[g] = V0 + len(gid)
+    names += list(gid)
+    pp = np.array([[gid[a], gid[b]] for a, b in pos], np.int32)
+    parts = shards + [np.tile(pp, (rep, 1))] if rep else shards
+    pairs = np.concatenate(parts)
+    del shards, parts
+    return pairs, names, pos
+
+
+def synthetic_gmt(path, pos, n_paths=300, max_genes=40, seed=0):
+    """pathways = a gene and its positive-pair neighbours (>= 4 of them)"""
+    nb = {}
+    for a, b in pos:
+        nb.setdefault(a, set()).add(b)
+        nb.setdefault(b, set()).add(a)
+    rng = np.random.RandomState(seed)
+    cands = sorted(g for g, s in nb.items() if len(s) >= 4)
+    pick = rng.choice(len(cands), size=min(n_paths, len(cands)), replace=False)
+    with open(path, "w") as f:
+        for k, i in enumerate(pick):
+            g = cands[i]
+            genes = [g] + sorted(nb[g])[:max_genes - 1]
+            f.write("\t".join([f"PATH{k}", "http://synthetic"] + genes) + "\n")
+
+
+def heldin(s0, s1, tok, counts, K, n=50000, seed=99):
+    rng = np.random.Generator(np.random.PCG64(seed))
+    idx = rng.integers(0, len(tok) // 2, n)
+    c, j = tok[2 * idx], tok[2 * idx + 1]
+    p = counts.astype(np.float64) ** 0.75
+    negs = rng.choice(len(counts), size=(n, K), p=p / p.sum())
+    u = s0[j].astype(np.float64)
+    pos = np.einsum("nd,nd->n", u, s1[c].astype(np.float64))
+    neg = np.einsum("nd,nkd->nk", u, s1[negs].astype(np.float64))
+    return float((np.logaddexp(0, -pos) + np.logaddexp(0, neg).sum(1)).mean())
+
+
+def export_and_score(tag, s0, index2word, counts, pos_genes, gmt, out, auc_seeds, D):
+    from gene2vec_amd import evaluate as EV
+    from gene2vec_amd import ggipnn as G
+    from gene2vec_amd.word2vec import KeyedVectors, Vocab
+    kv = KeyedVectors(D)
+    kv.index2word = list(index2word)
+    kv.vocab = {w: Vocab(count=int(counts[i]), index=i) for i, w in enumerate(index2word)}
+    kv.vectors = np.ascontiguousarray(s0, np.float32)
+    w2v = os.path.join(out, f"{tag}_w2v.txt")
+    kv.save_word2vec_format(w2v)
+    t = EV.target_function(w2v, gmt, strict=False, verbose=False)
+    txt = os.path.join(out, f"{tag}.txt")
+    with open(txt, "w") as f:  # generateMatrix layout, the GGIPNN genes only
+        for i, w in enumerate(index2word):
+            if w in pos_genes:
+                f.write(w + "\t" + "".join(v + " " for v in s0[i].astype(np.float32).astype(str))
+                        + "\n")
+    aucs = [G.train_and_auc(txt, DATA, seed=s, device="cuda") for s in auc_seeds]
+    return {"target_ratio": t["ratio"], "path_mean": t["path_mean"], "rand_mean": t["rand_mean"],
+            "n_pathways": t["n_pathways"], "auc": aucs, "auc_mean": float(np.mean(aucs))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--replicas", type=int, default=8)
+    ap.add_argument("--pairs-per-replica", type=int, default=125_000_000)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--merge-every", default="1024", help="comma-separated job cadences")
+    ap.add_argument("--vocab", type=int, default=24447)
+    ap.add_argument("--dim", type=int, default=200)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--sample", type=float, default=1e-3)
+    ap.add_argument("--ggipnn-repeat", type=int, default=30)
+    ap.add_argument("--auc-seeds", default="0,1,2")
+    ap.add_argument("--no-single", action="store_true")
+    ap.add_argument("--out", default="gpurun_out/replica_quality")
+    a = ap.parse_args()
+    import torch
+    os.makedirs(a.out, exist_ok=True)
+    R, D, K = a.replicas, a.dim, a.negative
+    t0 = time.time()
+    pairs, names, pos = build_corpus(R, a.pairs_per_replica, a.vocab, a.ggipnn_repeat, 5)
+    n = len(pairs)
+    flat = pairs.reshape(-1)
+    del pairs
+    counts, first = E.count_ids(flat, len(names))
+    order, remap = S.vocab_order(counts, first)
+    tok = remap[flat]
+    del flat
+    vc = counts[order].astype(np.int64)
+    V = len(order)
+    index2word = [names[i] for i in order]
+    pos_genes = {g for p in pos for g in p}
+    gmt = os.path.join(a.out, "synthetic.gmt")
+    synthetic_gmt(gmt, pos)
+    seeds = np.array([zlib.crc32((w + "1").encode()) for w in index2word], np.uint32)
+    syn0 = E.seeded_vectors(seeds, D)
+    dev = torch.device("cuda", 0)
+    base = torch.from_numpy(tok.view(np.int64)).to(dev)  # one pair per 8-byte item
+    perm = torch.empty_like(base)
+    rs_perm = np.random.RandomState(11)
+    perm_seeds = [int(rs_perm.randint(0, 2 ** 62)) for _ in range(a.iters)]
+    log = {"config": {"replicas": R, "pairs_per_replica": a.pairs_per_replica,
+                      "ggipnn_repeat": a.ggipnn_repeat, "pairs_total": n, "vocab": V,
+                      "dim": D, "negative": K, "sample": a.sample, "iters": a.iters},
+           "corpus_s": round(time.time() - t0, 1), "runs": {}}
+    print(json.dumps(log["config"]), flush=True)
+    st = torch.cuda.current_stream(dev)
+
+    def permute(it):
+        E.permute_items8(0, base.data_ptr(), perm.data_ptr(), n, 0, n, perm_seeds[it],
+                         st.cuda_stream)
+        st.synchronize()
+
+    def finish(tag, s0, s1, extra):
+        res = {"heldin": round(heldin(s0, s1, tok, vc, K), 5)}
+        res.update(export_and_score(tag, s0, index2word, vc, pos_genes, gmt, a.out,
+                                    [int(x) for x in a.auc_seeds.split(",")], D))
+        res.update(extra)
+        log["runs"][tag] = res
+        print(tag, json.dumps(res), flush=True)
+        json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
+
+    # ---- one model over the whole corpus ----------------------------------------
+    if not a.no_single:
+        eng = E.SGNSEngine(V, D, K)
+        eng.set_vocab(vc, a.sample)
+        eng.set_weights(syn0, np.zeros_like(syn0))
+        rs = np.random.RandomState(1)
+        js = E.plan_jobs(n_sent=n, sent_len=2)
+        al = E.job_alphas(js, n)
+        t = time.time()
+        per_it = []
+        for it in range(a.iters):
+            permute(it)
+            eng.set_corpus_device(perm.data_ptr(), 2 * n, sent_len=2, keepalive=perm)
+            eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)
+            eng.sync()
+            g0, g1 = eng.get_weights()
+            per_it.append(round(heldin(g0, g1, tok, vc, K, n=20000), 5))
+            print("single iter", it, per_it[-1], flush=True)
+        s0, s1 = eng.get_weights()
+        eng.close()
+        finish("single", s0, s1, {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
+
+    # ---- R replicas, libg2v merge every c jobs ---------------------------------------
+    for every in [int(x) for x in a.merge_every.split(",")]:
+        grp = E.LocalGroup(R)
+        agree = Dd.ThreadAgreement(R)
+        engs = []
+        for r in range(R):
+            e = E.SGNSEngine(V, D, K)
+            e.set_vocab(vc, a.sample)
+            e.set_weights(syn0, np.zeros_like(syn0))
+            engs.append(e)
+        with ThreadPoolExecutor(max_workers=R) as ex:
+            list(ex.map(lambda r: engs[r].comm_init_local(grp, r), range(R)))
+        trainers = [Dd.ReplicaTrainer(engs[r], (), every, N.MODE_HOGWILD, backend="libg2v",
+                                      world=R, agree=agree.for_rank(r)) for r in range(R)]
+        rs = np.random.RandomState(1)  # model.random, identical on every rank
+        t = time.time()
+        per_it = []
+        for it in range(a.iters):
+            permute(it)
+            base_seed = int(rs.randint(0, 2 ** 31 - 1))
+
+            def rank(r):
+                s0r, s1r = Dd.shard_range(n, r, R)
+                e = engs[r]
+                e.set_corpus_device(perm.data_ptr() + 8 * s0r, 2 * (s1r - s0r), sent_len=2,
+                                    keepalive=perm)
+                js = E.plan_jobs(n_sent=s1r - s0r, sent_len=2)
+                al = E.job_alphas(js, s1r - s0r)
+                sd = E.job_seeds(np.random.RandomState((base_seed + 7919 * r) % 2 ** 32),
+                                 len(js) - 1)
+                trainers[r].train_epoch(js, al, sd)
+                e.sync()
+            with ThreadPoolExecutor(max_workers=R) as ex:
+                list(ex.map(rank, range(R)))
+            g0, g1 = engs[0].get_weights()
+            per_it.append(round(heldin(g0, g1, tok, vc, K, n=20000), 5))
+            print(f"replicas x{R} every {every} iter {it} {per_it[-1]}", flush=True)
+        s0, s1 = engs[0].get_weights()
+        same = all(np.array_equal(e.get_weights()[0], s0) for e in engs[1:])
+        merges = trainers[0].averages
+        for e in engs:
+            e.close()
+        grp.close()
+        finish(f"replicas{R}_every{every}", s0, s1,
+               {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it,
+                "merges_total": merges, "replicas_identical": same})
+    if "single" in log["runs"]:
+        ref = log["runs"]["single"]
+        for tag, r in log["runs"].items():
+            if tag != "single":
+                r["heldin_gap"] = round((r["heldin"] - ref["heldin"]) / ref["heldin"], 5)
+                r["auc_gap"] = round((r["auc_mean"] - ref["auc_mean"]) / ref["auc_mean"], 5)
+                r["target_gap"] = round((r["target_ratio"] - ref["target_ratio"])
+                                        / ref["target_ratio"], 5)
+        json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
+    print(json.dumps(log))
+
+
+if __name__ == "__main__":
+    main()

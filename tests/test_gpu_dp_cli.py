@@ -5,9 +5,9 @@ one process, src/gene2vec.py:59).  The round's box has one GPU, so two ranks
 share cuda:0 over gloo here: the merge is libg2v's own (delta/apply kernels,
 in-call merges, rank-0 broadcast), its all-reduce carried by gloo through the
 host (--merge-transport host, the gloo default); the 8-GPU node runs the same
-merge over RCCL.  One test keeps the torch-tensor merge (--merge-transport torch).  Checks: rank 0 alone writes the outputs every rank reloads, and the
-model's held-in SGNS objective improves at least 93 % as much as the
-single-process run's (measured 97 %)."""
+merge over RCCL.  One test keeps the torch-tensor merge (--merge-transport
+torch).  Checks: rank 0 alone writes the outputs every rank reloads, and the
+model's held-in SGNS objective lands within 2 % of the single-process run's."""
 import os
 import socket
 import subprocess
@@ -80,11 +80,12 @@ def test_cli_data_parallel_two_ranks(tmp_path):
     l1, l2 = _heldin_loss(single, pairs, names), _heldin_loss(dp, pairs, names)
     print("held-in SGNS objective: init %.4f single %.4f data-parallel %.4f" % (init, l1, l2))
     assert l1 < 0.9 * init and l2 < 0.9 * init
-    # model averaging halves the step of rows both replicas train between merges
-    # (distributed.touch_merge_): the replicas learn a little slower than one
-    # process on a corpus this small; bar: 93 % of the single run's improvement
-    # (measured 2.8221 vs 2.7867 = 97 %)
-    assert (init - l2) >= 0.93 * (init - l1), (l1, l2)
+    # the touch merge averages the deltas of rows both replicas trained between
+    # merges (distributed.touch_merge_): on a corpus this small, merged every 8
+    # jobs, the replicas learn a little slower than one process (round 2:
+    # 2.8221 vs 2.7867, +1.3 %); bar: the data-parallel objective within 2 %
+    # of the single run's
+    assert (l2 - l1) / l1 < 0.02, (l1, l2)
 
 
 def test_cli_data_parallel_replicas_identical(tmp_path):

@@ -112,14 +112,14 @@ def test_loss_hogwild_tracks_sequential():
     here), while the Hogwild tally adds per-wave float partials of 32
     examples in double.  The tally prices each prediction before its update,
     so the ~2,000 examples in flight show while the model learns fast.
-    Bars: iteration 1 within 3 %, iteration 2 within 1.5 %."""
+    Bars: iteration 1 within 1.5 %, iteration 2 within 1 %."""
     D, K = 200, 5
     tok, counts, syn0 = _zipf(2_000_000, 24447, D)
     got, g0, g1 = _run(tok, counts, syn0, K, 1e-3, N.MODE_HOGWILD, True, iters=2)
     ref, _, _ = _oracle(tok, counts, syn0, K, 1e-3, iters=2, exact=True)
     print("hogwild loss", got, "sequential oracle", ref)
-    assert abs(got[0] - ref[0]) / ref[0] < 0.03, (got, ref)
-    assert abs(got[1] - ref[1]) / ref[1] < 0.015, (got, ref)
+    assert abs(got[0] - ref[0]) / ref[0] < 0.015, (got, ref)
+    assert abs(got[1] - ref[1]) / ref[1] < 0.01, (got, ref)
     assert np.isfinite(g0).all() and np.isfinite(g1).all()
 
 

@@ -278,7 +278,8 @@ def test_train_sequential_vs_c_oracle_zipf(seg_jobs):
 def test_train_tiny_vocabulary(V, mode):
     """degenerate vocabularies: one gene (every negative equals the center and
     is skipped), two and three genes; sequential vs the C oracle at 1e-5,
-    Hogwild: identical counts and finite tables"""
+    Hogwild: identical counts and the pair objective within 1 % of the
+    sequential oracle's"""
     D, K, sample = 16, 5, 1e-3
     rng = np.random.RandomState(V)
     n = 3000
@@ -310,6 +311,33 @@ def test_train_tiny_vocabulary(V, mode):
     if mode == "sequential":
         _close(g0, a0, atol=1e-6)
         _close(g1, a1, atol=1e-6)
+    else:
+        # Hogwild on 1-3 rows: every example in flight shares the rows; the
+        # staleness-bounded grid keeps the learned objective at the sequential
+        # oracle's (the same corpus pairs, gensim's negatives skipped when they
+        # equal the centre)
+        got = _pair_objective(g0, g1, tok, counts, K)
+        exp = _pair_objective(a0, a1, tok, counts, K)
+        init = _pair_objective(syn0, np.zeros((V, D), np.float32), tok, counts, K)
+        print("tiny vocabulary V=%d: init %.5f hogwild %.5f sequential %.5f" % (V, init, got, exp))
+        assert exp < init
+        assert abs(got - exp) / exp < 0.01, (got, exp)
+
+
+def _pair_objective(syn0, syn1, tok, counts, K, seed=3):
+    """SGNS objective over every directed pair of the corpus: -log s(u.v_c) -
+    sum over K unigram^0.75 negatives (skipped when equal to the centre) of
+    log s(-u.v_n), in double"""
+    rng = np.random.RandomState(seed)
+    c, j = tok[0::2], tok[1::2]
+    c, j = np.concatenate([c, j]), np.concatenate([j, c])
+    p = counts.astype(np.float64) ** 0.75
+    negs = rng.choice(len(counts), size=(len(c), K), p=p / p.sum())
+    u = syn0[j].astype(np.float64)
+    pos = np.einsum("nd,nd->n", u, syn1[c].astype(np.float64))
+    neg = np.einsum("nd,nkd->nk", u, syn1[negs].astype(np.float64))
+    keep = negs != c[:, None]
+    return float((np.logaddexp(0, -pos) + (np.logaddexp(0, neg) * keep).sum(1)).mean())
 
 
 def _eval_loss(syn0, syn1, tok, counts, K, n_eval=20000, seed=99):
@@ -330,7 +358,7 @@ def test_train_hogwild_objective_matches_oracle(D, K, seg_jobs, overlap):
     updates; it is judged end-to-end).  Measured at the
     default grid over 5 seed streams: -0.06..+0.11 %, mean +0.05 %; the
     sequential oracle's own seed-to-seed spread is 0.5 %
-    (profiles/r02_hogwild_dev.log).  overlap = G2V_OPT_ATOMIC_OVERLAP."""
+    (profiles/r02/r02_pipeline/hogwild_dev_*.log).  overlap = G2V_OPT_ATOMIC_OVERLAP."""
     sample = 1e-3
     tok, counts, syn0 = _zipf_setup(200000, 3000, D, K, sample)
     V = len(counts)
