@@ -112,8 +112,9 @@ def build_examples(verbose=False):
     src = os.path.join(EXAMPLES, "g2v_train.c")
     out = os.path.join(EXAMPLES, "g2v_train")
     lib = os.path.join(HERE, "libg2v.so")
-    if (os.path.exists(out) and os.path.getmtime(out) >= os.path.getmtime(src)
-            and os.path.getmtime(out) >= os.path.getmtime(lib)):
+    header = os.path.join(os.path.dirname(HERE), "include", "g2v.h")
+    if (os.path.exists(out)
+            and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in (src, lib, header))):
         return out
     cmd = ["gcc", "-O2", "-std=c11", "-Wall", "-Wextra",
            "-I", os.path.join(os.path.dirname(HERE), "include"), src, "-L", HERE, "-lg2v",
