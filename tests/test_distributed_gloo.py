@@ -32,6 +32,26 @@ class FakeEngine:
             t += float((self.rank + 1) * len(al))
 
 
+class FailingEngine:
+    """libg2v-backend stand-in: train raises on one rank, average / abort recorded"""
+
+    def __init__(self, fail):
+        self.fail, self.aborted, self.opts, self.averages = fail, False, {}, 0
+
+    def set_option(self, k, v):
+        self.opts[k] = v
+
+    def train(self, js, al, sd, mode, timing=False, compute_loss=False):
+        if self.fail:
+            raise RuntimeError("boom")
+
+    def average(self, rule):
+        self.averages += 1
+
+    def comm_abort(self):
+        self.aborted = True
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -95,6 +115,27 @@ def _worker(rank, world, port, q):
         out["uneven_calls"] = eng2.calls
         out["uneven_averages"] = tr2.averages
         out["uneven_tables"] = tabs2[0].numpy()
+        # g2v_comm_init_host's collective over gloo: rank-order sum, broadcast
+        from gene2vec_amd import _native as N
+        coll = Dd.host_collective()
+        a = np.array([0.1, 1e8, -3.0, 7.0], np.float32) * np.float32(rank + 1)
+        coll(N.COLL_SUM, a)
+        out["coll_sum"] = a
+        b = np.full(3, 10.0 * (rank + 1), np.float32)
+        coll(N.COLL_BCAST0, b)
+        out["coll_bcast"] = b
+        # libg2v backend: a rank whose epoch fails re-raises its error, its peer
+        # learns of it from the ok-flag agreement and leaves the communicator
+        fe = FailingEngine(fail=(rank == 1))
+        tr3 = Dd.ReplicaTrainer(fe, (), avg_every_jobs=4, backend="libg2v")
+        try:
+            tr3.train_epoch(np.arange(0, 21, 2, dtype=np.int64), np.zeros(10),
+                            np.zeros(10, np.uint64))
+            out["fail"] = None
+        except RuntimeError as e:
+            out["fail"] = str(e)
+        out["aborted"] = fe.aborted
+        out["merge_every_reset"] = fe.opts.get(N.OPT_MERGE_EVERY_JOBS)
         out["max_int"] = Dd.allreduce_max_int(5 + rank)
         out["sum_float"] = Dd.allreduce_sum_float(0.5 * (rank + 1))
         q.put((rank, out))
@@ -172,6 +213,37 @@ def test_uneven_shards_same_merge_count(results):
     # window adds: rank 0 4, 4, 2; rank 1 8, 4, 0 -> means 6, 4, 1 -> 11
     assert np.array_equal(results[0]["uneven_tables"], results[1]["uneven_tables"])
     assert np.allclose(results[0]["uneven_tables"], 11.0)
+
+
+def test_host_collective_rank_order_sum_and_broadcast(results):
+    a = np.array([0.1, 1e8, -3.0, 7.0], np.float32)
+    expect = np.zeros(4, np.float32) + a + a * np.float32(2)
+    for r in (0, 1):
+        assert np.array_equal(results[r]["coll_sum"], expect)
+        assert np.array_equal(results[r]["coll_bcast"], np.full(3, 10.0, np.float32))
+
+
+def test_libg2v_backend_failure_reaches_every_rank(results):
+    assert results[1]["fail"] == "boom" and not results[1]["aborted"]
+    assert "another rank" in results[0]["fail"] and results[0]["aborted"]
+    for r in (0, 1):
+        assert results[r]["merge_every_reset"] == 0
+
+
+def test_thread_agreement_min():
+    import threading
+    ag = Dd.ThreadAgreement(3)
+    got = [None] * 3
+
+    def run(r):
+        f = ag.for_rank(r)
+        got[r] = (f(5 - r), f(10 + r))
+    th = [threading.Thread(target=run, args=(r,)) for r in range(3)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=30)
+    assert got == [(3, 10)] * 3
 
 
 def test_scalar_agreements(results):
