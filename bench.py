@@ -279,6 +279,10 @@ def main():
     # examples per launch; a profile of another build is refused (traffic null)
     from gene2vec_amd.build import kernel_source_hash
     ksha = kernel_source_hash()
+    launch = {"grid_workgroups": eng.get_option(N.OPT_GRID),
+              "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}",
+              "stripes_tier2": f"rows < {eng.get_option(N.OPT_STRIPE2_ROWS)} "
+                               f"x{eng.get_option(N.OPT_STRIPE2_COPIES)}"}
     cands = [a.traffic_json] if a.traffic_json else sorted(
         glob.glob(os.path.join(ROOT, "profiles", "**", "traffic_r*.json"), recursive=True),
         reverse=True)
@@ -293,16 +297,18 @@ def main():
         if (tj.get("vocab"), tj.get("dim"), tj.get("negative"), tj.get("sample"),
                 tj.get("zipf")) != (V0, D, K, a.sample, a.zipf):
             continue
-        if tj.get("kernel_src_sha16") != ksha:
+        if tj.get("kernel_src_sha16") != ksha or tj.get("launch") != launch:
             stale.append(os.path.relpath(tpath, ROOT))
             continue
         traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
                         * st["examples"] / launches, 1)
-        traffic_src = (f"{os.path.relpath(tpath, ROOT)} (kernel build {ksha}): PMC bytes "
+        traffic_src = (f"{os.path.relpath(tpath, ROOT)} (kernel build {ksha}, same launch "
+                       "layout): PMC bytes "
                        f"per example x this run's {st['examples'] // launches} examples per "
                        "launch (not measured in this process)")
     if traffic is None:
-        traffic_src = (f"no PMC profile of kernel build {ksha} for this workload"
+        traffic_src = (f"no PMC profile of kernel build {ksha} with this launch layout for "
+                       "this workload"
                        + (f"; refused profiles of other builds: {', '.join(stale[:3])}"
                           if stale else ""))
     atomic_bytes = (K + 2) * D * 4  # every SGNS update is a memory-side f32 atomic delta
@@ -318,10 +324,7 @@ def main():
                 "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
                 "atomic_frac": round(atomic_gbps / 1300.0, 4), "traffic_source": traffic_src,
                 "kernel_src_sha16": ksha,
-                "grid_workgroups": eng.get_option(N.OPT_GRID),
-                "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}",
-                "stripes_tier2": f"rows < {eng.get_option(N.OPT_STRIPE2_ROWS)} "
-                                 f"x{eng.get_option(N.OPT_STRIPE2_COPIES)}"}
+                **launch}
 
     # ---- measured gather roof: the same kernel on the same index
     # stream with its table writes compiled out (G2V_OPT_DEBUG_WRITE=2) and a

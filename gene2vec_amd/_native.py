@@ -45,6 +45,7 @@ OPT_MERGE_RULE = 12
 OPT_STRIPE2_ROWS = 13
 OPT_STRIPE2_COPIES = 14
 OPT_ACTIVE_WAVES = 15
+OPT_MERGE_BETA_MILLI = 16
 COLL_SUM = 0
 COLL_BCAST0 = 1
 BATCH_WORDS = 10000

@@ -26,10 +26,11 @@ SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(CSRC, "g2v_device.h"),
            os.path.join(ROOT, "include", "g2v.h")]
 ARCH = "gfx950"
-# the sources that determine k_sgns_atomic's code and launch (bench.py accepts a
-# PMC traffic profile only when it was measured on this exact kernel build)
+# the sources that determine k_sgns_atomic's code (bench.py accepts a PMC
+# traffic profile only when it was measured on this exact kernel code AND the
+# same launch layout: grid and stripe tiers, recorded beside the hash)
 KERNEL_SOURCES = [os.path.join(CSRC, s) for s in
-                  ("g2v_sgns_atomic.hip", "g2v_device.h", "g2v_internal.h", "g2v_api.hip")]
+                  ("g2v_sgns_atomic.hip", "g2v_device.h", "g2v_internal.h")]
 
 
 def kernel_source_hash() -> str:

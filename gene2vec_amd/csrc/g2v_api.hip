@@ -144,6 +144,7 @@ struct g2v_ctx {
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int merge_rule = 0;
+  float merge_beta = 1.0f;  // G2V_OPT_MERGE_BETA_MILLI / 1000
   float* stripe = nullptr;
   int64_t stripe_cap = 0;
   uint32_t* dbg16 = nullptr;  // ablation 3: packed-f16 atomic scratch [2][V + stripes][ld/2]
@@ -637,6 +638,10 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->grid_user = value > 0;
       c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv, c->u_max);
       return G2V_OK;
+    case G2V_OPT_MERGE_BETA_MILLI:
+      REQUIRE(value >= 0 && value <= 1000, G2V_EINVAL, "merge beta (x1000) out of [0, 1000]");
+      c->merge_beta = (float)value / 1000.0f;
+      return G2V_OK;
     case G2V_OPT_ACTIVE_WAVES:
       REQUIRE(value >= 1 && value <= kSgnsThreads / 64, G2V_EINVAL, "active waves out of [1, %d]",
               kSgnsThreads / 64);
@@ -664,6 +669,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_MERGE_EVERY_JOBS: *out = c->merge_every; return G2V_OK;
     case G2V_OPT_MERGE_RULE: *out = c->merge_rule; return G2V_OK;
     case G2V_OPT_ACTIVE_WAVES: *out = c->active_waves; return G2V_OK;
+    case G2V_OPT_MERGE_BETA_MILLI: *out = (int64_t)lrintf(c->merge_beta * 1000.0f); return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -1836,7 +1842,7 @@ static int merge_now(g2v_ctx* c, int rule) {
   if (rc) return rc;
   for (int k = 0; k < 2; ++k)
     HIPCHK(launch_merge_apply(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
-                              rule, 1.0f / (float)c->nranks, c->stream));
+                              rule, 1.0f / (float)c->nranks, c->merge_beta, c->stream));
   return G2V_OK;
 }
 
@@ -1865,7 +1871,7 @@ int g2v_average_local(g2v_ctx* const* ctxs, int n, int rule) {
       a.t[i] = k ? ctxs[i]->syn1 : ctxs[i]->syn0;
       a.old[i] = k ? ctxs[i]->merge1 : ctxs[i]->merge0;
     }
-    HIPCHK(launch_merge_local(a, n, c0->V, c0->ld, c0->nvec, rule, c0->stream));
+    HIPCHK(launch_merge_local(a, n, c0->V, c0->ld, c0->nvec, rule, c0->merge_beta, c0->stream));
   }
   // later work on the other contexts' streams must see the merged tables
   bool other = false;

@@ -142,7 +142,7 @@ hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
                                int64_t ld, int nvec, hipStream_t st);
 // replica merge (g2v_average*): rows of one [V][ld] table per call
 //   delta:  t <- t - old; cnt[row] = any(t - old != 0)
-//   apply:  touch: old <- old + t / max(cnt, 1); mean: old <- t * inv_n;  t <- old
+//   apply:  touch: old <- old + t / max(cnt, 1)^beta; mean: old <- t * inv_n;  t <- old
 //   local:  the whole touch/mean merge over n replicas of one device
 constexpr int kMaxLocalReplicas = 16;
 struct LocalMergeArgs {
@@ -152,9 +152,9 @@ struct LocalMergeArgs {
 hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V, int64_t ld,
                               int nvec, hipStream_t st);
 hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V, int64_t ld,
-                              int nvec, int rule, float inv_n, hipStream_t st);
+                              int nvec, int rule, float inv_n, float beta, hipStream_t st);
 hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
-                              int rule, hipStream_t st);
+                              int rule, float beta, hipStream_t st);
 // in-process replica group (g2v_comm_init_local): dst = sum over n sources,
 // added in source order from 0.f (k_merge_local's order)
 struct SumArgs {

@@ -382,17 +382,23 @@ __global__ __launch_bounds__(256) void k_merge_delta(float* __restrict__ t,
 }
 
 // after the all-reduce: touch (rule 0) t holds sum_r d_r, cnt the number of
-// replicas that changed the row: new = old + t / max(cnt, 1); mean (rule 1)
-// t holds sum_r t_r: new = t * inv_n.  Both: old = t = new.
+// replicas that changed the row: new = old + t / max(cnt, 1)^beta (beta = 1:
+// the mean of the changes, 0: their sum); mean (rule 1) t holds sum_r t_r:
+// new = t * inv_n.  Both: old = t = new.
+__device__ __forceinline__ float touch_div(float k, float beta) {
+  return beta == 1.f ? k : powf(k, beta);
+}
+
 __global__ __launch_bounds__(256) void k_merge_apply(float* __restrict__ t, float* __restrict__ old,
                                                      const float* __restrict__ cnt, int64_t V,
-                                                     int64_t ld, int nvec, int rule, float inv_n) {
+                                                     int64_t ld, int nvec, int rule, float inv_n,
+                                                     float beta) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= V) return;
   float4* tr = reinterpret_cast<float4*>(t + r * ld);
   float4* orw = reinterpret_cast<float4*>(old + r * ld);
-  const float k = rule == 0 ? fmaxf(cnt[r], 1.f) : 1.f;
+  const float k = rule == 0 ? touch_div(fmaxf(cnt[r], 1.f), beta) : 1.f;
   for (int c = lane; c < nvec; c += 64) {
     const float4 x = tr[c];
     float4 nv;
@@ -410,7 +416,7 @@ __global__ __launch_bounds__(256) void k_merge_apply(float* __restrict__ t, floa
 // n replicas on one device: the whole merge in one pass (deltas summed in
 // replica order)
 __global__ __launch_bounds__(256) void k_merge_local(LocalMergeArgs a, int n, int64_t V,
-                                                     int64_t ld, int nvec, int rule) {
+                                                     int64_t ld, int nvec, int rule, float beta) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= V) return;
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(256) void k_merge_local(LocalMergeArgs a, int n, in
       k += __any(nz) ? 1 : 0;
     }
   }
-  const float kf = k > 1 ? (float)k : 1.f;
+  const float kf = touch_div(k > 1 ? (float)k : 1.f, beta);
   const float inv_n = 1.f / (float)n;
   for (int c = lane; c < nvec; c += 64) {
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -514,18 +520,18 @@ hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V,
 }
 
 hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V, int64_t ld,
-                              int nvec, int rule, float inv_n, hipStream_t st) {
+                              int nvec, int rule, float inv_n, float beta, hipStream_t st) {
   if (V <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_merge_apply, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, old, cnt,
-                     V, ld, nvec, rule, inv_n);
+                     V, ld, nvec, rule, inv_n, beta);
   return hipGetLastError();
 }
 
 hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
-                              int rule, hipStream_t st) {
+                              int rule, float beta, hipStream_t st) {
   if (V <= 0 || n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_merge_local, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, a, n, V, ld,
-                     nvec, rule);
+                     nvec, rule, beta);
   return hipGetLastError();
 }
 

@@ -52,10 +52,11 @@ def main(out):
     res = {
         # the kernel build these counters belong to (bench.py refuses any other)
         "kernel_src_sha16": kernel_source_hash(),
+        "launch": {k: b["roofline"][k] for k in ("grid_workgroups", "stripes", "stripes_tier2")},
         "vocab": cfg.get("vocab_requested", cfg["vocab"]), "dim": cfg["dim"], "negative": cfg["negative"],
         "sample": cfg["sample"], "zipf": cfg.get("zipf", 1.0), "kernel": KERNEL,
         "method": "rocprofv3 --pmc, one counter group per run (scripts/profile_round.sh), "
-                  "10 M-pair bench; FETCH_SIZE x2 (gfx950 16-B/lane read correction), "
+                  "one-step bench of the workload; FETCH_SIZE x2 (gfx950 16-B/lane read correction), "
                   "WRITE_SIZE as is (KB units); summed over the SGNS launches / examples",
         "fetch_bytes_per_example": fetch, "write_bytes_per_example": write,
         "atomic_requests_per_example": c.get("TCC_EA0_ATOMIC_sum", 0.0) / ex,

@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round evidence on the GPU box: rocprofv3 kernel stats of the bench command,
 # then the PMC passes (one counter group per run, --kernel-trace-free) over a
-# 10 M-pair bench whose per-example bytes feed roofline.traffic.
+# one-step bench of the same workload (same vocabulary counts, so the same
+# default grid and stripes) whose per-example bytes feed roofline.traffic.
 #   usage: scripts/profile_round.sh r02 [extra bench args, e.g. the C4 shape, for every run]
 set -e
 R=${1:?round tag}
@@ -12,7 +13,7 @@ mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o bench --output-format csv \
   -- python3 bench.py --no-cpu-baseline "$@" > "$OUT/bench_stats.log" 2>&1
 echo "stats pass rc=$?"
-ARGS="--pairs 10000000 --steps 1 --warmup 0 --no-cpu-baseline --no-eval --no-gather-roof $*"
+ARGS="--steps 1 --warmup 0 --no-cpu-baseline --no-eval --no-gather-roof $*"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVES" "TCC_EA0_RDREQ_DRAM_sum TCC_EA0_WRREQ_ATOMIC_DRAM_sum"; do
   i=$((i+1))

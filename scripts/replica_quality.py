@@ -136,6 +136,10 @@ def main():
     ap.add_argument("--pairs-per-replica", type=int, default=125_000_000)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--merge-every", default="1024", help="comma-separated job cadences")
+    ap.add_argument("--betas", default="1000",
+                    help="comma-separated touch-rule exponents x 1000 (G2V_OPT_MERGE_BETA_MILLI)")
+    ap.add_argument("--no-eval", action="store_true",
+                    help="held-in objective only (no exports, target function, GGIPNN)")
     ap.add_argument("--vocab", type=int, default=24447)
     ap.add_argument("--dim", type=int, default=200)
     ap.add_argument("--negative", type=int, default=5)
@@ -184,8 +188,9 @@ def main():
 
     def finish(tag, s0, s1, extra):
         res = {"heldin": round(heldin(s0, s1, tok, vc, K), 5)}
-        res.update(export_and_score(tag, s0, index2word, vc, pos_genes, gmt, a.out,
-                                    [int(x) for x in a.auc_seeds.split(",")], D))
+        if not a.no_eval:
+            res.update(export_and_score(tag, s0, index2word, vc, pos_genes, gmt, a.out,
+                                        [int(x) for x in a.auc_seeds.split(",")], D))
         res.update(extra)
         log["runs"][tag] = res
         print(tag, json.dumps(res), flush=True)
@@ -214,7 +219,8 @@ def main():
         finish("single", s0, s1, {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
 
     # ---- R replicas, libg2v merge every c jobs ---------------------------------------
-    for every in [int(x) for x in a.merge_every.split(",")]:
+    combos = [(int(e), int(b)) for e in a.merge_every.split(",") for b in a.betas.split(",")]
+    for every, beta in combos:
         grp = E.LocalGroup(R)
         agree = Dd.ThreadAgreement(R)
         engs = []
@@ -222,6 +228,7 @@ def main():
             e = E.SGNSEngine(V, D, K)
             e.set_vocab(vc, a.sample)
             e.set_weights(syn0, np.zeros_like(syn0))
+            e.set_option(N.OPT_MERGE_BETA_MILLI, beta)
             engs.append(e)
         with ThreadPoolExecutor(max_workers=R) as ex:
             list(ex.map(lambda r: engs[r].comm_init_local(grp, r), range(R)))
@@ -249,14 +256,14 @@ def main():
                 list(ex.map(rank, range(R)))
             g0, g1 = engs[0].get_weights()
             per_it.append(round(heldin(g0, g1, tok, vc, K, n=20000), 5))
-            print(f"replicas x{R} every {every} iter {it} {per_it[-1]}", flush=True)
+            print(f"replicas x{R} every {every} beta {beta} iter {it} {per_it[-1]}", flush=True)
         s0, s1 = engs[0].get_weights()
         same = all(np.array_equal(e.get_weights()[0], s0) for e in engs[1:])
         merges = trainers[0].averages
         for e in engs:
             e.close()
         grp.close()
-        finish(f"replicas{R}_every{every}", s0, s1,
+        finish(f"replicas{R}_every{every}" + (f"_beta{beta}" if beta != 1000 else ""), s0, s1,
                {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it,
                 "merges_total": merges, "replicas_identical": same})
     if "single" in log["runs"]:
@@ -264,10 +271,14 @@ def main():
         for tag, r in log["runs"].items():
             if tag != "single":
                 r["heldin_gap"] = round((r["heldin"] - ref["heldin"]) / ref["heldin"], 5)
-                r["auc_gap"] = round((r["auc_mean"] - ref["auc_mean"]) / ref["auc_mean"], 5)
-                r["target_gap"] = round((r["target_ratio"] - ref["target_ratio"])
-                                        / ref["target_ratio"], 5)
+                if "auc_mean" in r and "auc_mean" in ref:
+                    r["auc_gap"] = round((r["auc_mean"] - ref["auc_mean"]) / ref["auc_mean"], 5)
+                    r["target_gap"] = round((r["target_ratio"] - ref["target_ratio"])
+                                            / ref["target_ratio"], 5)
         json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
+    for tag, r in log["runs"].items():
+        print(tag, {k: r[k] for k in ("heldin", "heldin_gap", "auc_mean", "auc_gap",
+                                      "target_ratio", "target_gap") if k in r})
     print(json.dumps(log))
 
 
