@@ -28,6 +28,7 @@ FLAG_TIMING = 0x100
 FLAG_COMPUTE_LOSS = 0x200
 MERGE_TOUCH = 0
 MERGE_MEAN = 1
+MERGE_ALIGN = 2
 UNIQUE_ID_BYTES = 128
 CORPUS_DEVICE = 0x1
 OPT_HOT_ROWS = 1
@@ -46,6 +47,7 @@ OPT_STRIPE2_ROWS = 13
 OPT_STRIPE2_COPIES = 14
 OPT_ACTIVE_WAVES = 15
 OPT_MERGE_BETA_MILLI = 16
+OPT_MERGE_GAMMA_MILLI = 17
 COLL_SUM = 0
 COLL_BCAST0 = 1
 BATCH_WORDS = 10000

@@ -144,7 +144,8 @@ struct g2v_ctx {
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int merge_rule = 0;
-  float merge_beta = 1.0f;  // G2V_OPT_MERGE_BETA_MILLI / 1000
+  float merge_beta = 1.0f;   // G2V_OPT_MERGE_BETA_MILLI / 1000
+  float merge_gamma = 1.0f;  // G2V_OPT_MERGE_GAMMA_MILLI / 1000
   float* stripe = nullptr;
   int64_t stripe_cap = 0;
   uint32_t* dbg16 = nullptr;  // ablation 3: packed-f16 atomic scratch [2][V + stripes][ld/2]
@@ -629,8 +630,8 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->merge_every = value;
       return G2V_OK;
     case G2V_OPT_MERGE_RULE:
-      REQUIRE(value == G2V_MERGE_TOUCH || value == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %lld",
-              (long long)value);
+      REQUIRE(value == G2V_MERGE_TOUCH || value == G2V_MERGE_MEAN || value == G2V_MERGE_ALIGN,
+              G2V_EINVAL, "merge rule %lld", (long long)value);
       c->merge_rule = (int)value;
       return G2V_OK;
     case G2V_OPT_GRID:
@@ -641,6 +642,11 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
     case G2V_OPT_MERGE_BETA_MILLI:
       REQUIRE(value >= 0 && value <= 1000, G2V_EINVAL, "merge beta (x1000) out of [0, 1000]");
       c->merge_beta = (float)value / 1000.0f;
+      return G2V_OK;
+    case G2V_OPT_MERGE_GAMMA_MILLI:
+      REQUIRE(value >= 1000 && value <= 16000, G2V_EINVAL,
+              "merge gamma (x1000) out of [1000, 16000]");
+      c->merge_gamma = (float)value / 1000.0f;
       return G2V_OK;
     case G2V_OPT_ACTIVE_WAVES:
       REQUIRE(value >= 1 && value <= kSgnsThreads / 64, G2V_EINVAL, "active waves out of [1, %d]",
@@ -670,6 +676,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_MERGE_RULE: *out = c->merge_rule; return G2V_OK;
     case G2V_OPT_ACTIVE_WAVES: *out = c->active_waves; return G2V_OK;
     case G2V_OPT_MERGE_BETA_MILLI: *out = (int64_t)lrintf(c->merge_beta * 1000.0f); return G2V_OK;
+    case G2V_OPT_MERGE_GAMMA_MILLI: *out = (int64_t)lrintf(c->merge_gamma * 1000.0f); return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -1480,7 +1487,7 @@ int g2v_merge_snapshot(g2v_ctx* c) {
     dev_free(c->merge1);
     dev_free(c->merge_cnt);
     if ((rc = dev_alloc(&c->merge0, tab)) || (rc = dev_alloc(&c->merge1, tab)) ||
-        (rc = dev_alloc(&c->merge_cnt, 2 * (size_t)c->V)))
+        (rc = dev_alloc(&c->merge_cnt, 4 * (size_t)c->V)))  // [cnt0, cnt1, nsq0, nsq1]
       return rc;
     c->merge_ld = c->ld;
   }
@@ -1569,7 +1576,7 @@ int g2v_comm_init_local(g2v_ctx* c, g2v_local_group* g, int rank) {
     if (rank == 0) {
       HIPCHK(hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming));
       // both tables and both touched-count vectors of one merge
-      const size_t need = 2 * (size_t)c->V * (size_t)c->ld + 2 * (size_t)c->V;
+      const size_t need = 2 * (size_t)c->V * (size_t)c->ld + 4 * (size_t)c->V;
       if ((rc = dev_alloc(&g->scratch, need))) return rc;
       g->scratch_cap = need;
     }
@@ -1609,7 +1616,8 @@ int g2v_comm_abort(g2v_ctx* c) {
 int g2v_average(g2v_ctx* c, int rule) {
   int rc = set_dev(c);
   if (rc) return rc;
-  REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %d", rule);
+  REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN || rule == G2V_MERGE_ALIGN, G2V_EINVAL,
+          "merge rule %d", rule);
   if (c->comm_kind == kCommNone) return G2V_OK;  // no communicator: nothing to merge with
   rc = merge_now(c, rule);
   if (rc) {
@@ -1832,17 +1840,21 @@ static int merge_now(g2v_ctx* c, int rule) {
   const size_t tab = (size_t)c->V * (size_t)c->ld;
   float* t[2] = {c->syn0, c->syn1};
   float* o[2] = {c->merge0, c->merge1};
-  if (rule == G2V_MERGE_TOUCH)
+  float* cnt = c->merge_cnt;                 // [2][V] touched flags, then counts
+  float* nsq = c->merge_cnt + 2 * (size_t)c->V;  // [2][V] squared delta norms, then sums
+  if (rule != G2V_MERGE_MEAN)
     for (int k = 0; k < 2; ++k)
-      HIPCHK(launch_merge_delta(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
-                                c->stream));
-  float* bufs[3] = {t[0], t[1], c->merge_cnt};
-  const size_t n[3] = {tab, tab, 2 * (size_t)c->V};
-  int rc = comm_allreduce(c, bufs, n, rule == G2V_MERGE_TOUCH ? 3 : 2);
+      HIPCHK(launch_merge_delta(t[k], o[k], cnt + (size_t)k * c->V, nsq + (size_t)k * c->V, c->V,
+                                c->ld, c->nvec, c->stream));
+  // one grouped collective: both tables, then the counts (and norms)
+  float* bufs[3] = {t[0], t[1], cnt};
+  const size_t n[3] = {tab, tab, (rule == G2V_MERGE_ALIGN ? 4 : 2) * (size_t)c->V};
+  int rc = comm_allreduce(c, bufs, n, rule == G2V_MERGE_MEAN ? 2 : 3);
   if (rc) return rc;
   for (int k = 0; k < 2; ++k)
-    HIPCHK(launch_merge_apply(t[k], o[k], c->merge_cnt + (size_t)k * c->V, c->V, c->ld, c->nvec,
-                              rule, 1.0f / (float)c->nranks, c->merge_beta, c->stream));
+    HIPCHK(launch_merge_apply(t[k], o[k], cnt + (size_t)k * c->V, nsq + (size_t)k * c->V, c->V,
+                              c->ld, c->nvec, rule, 1.0f / (float)c->nranks, c->merge_beta,
+                              c->merge_gamma, c->stream));
   return G2V_OK;
 }
 
@@ -1851,7 +1863,8 @@ extern "C" {
 int g2v_average_local(g2v_ctx* const* ctxs, int n, int rule) {
   REQUIRE(ctxs != nullptr && n >= 1 && n <= kMaxLocalReplicas, G2V_EINVAL,
           "need 1..%d contexts", kMaxLocalReplicas);
-  REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN, G2V_EINVAL, "merge rule %d", rule);
+  REQUIRE(rule == G2V_MERGE_TOUCH || rule == G2V_MERGE_MEAN || rule == G2V_MERGE_ALIGN, G2V_EINVAL,
+          "merge rule %d", rule);
   g2v_ctx* c0 = ctxs[0];
   int rc = set_dev(c0);
   if (rc) return rc;
@@ -1871,7 +1884,8 @@ int g2v_average_local(g2v_ctx* const* ctxs, int n, int rule) {
       a.t[i] = k ? ctxs[i]->syn1 : ctxs[i]->syn0;
       a.old[i] = k ? ctxs[i]->merge1 : ctxs[i]->merge0;
     }
-    HIPCHK(launch_merge_local(a, n, c0->V, c0->ld, c0->nvec, rule, c0->merge_beta, c0->stream));
+    HIPCHK(launch_merge_local(a, n, c0->V, c0->ld, c0->nvec, rule, c0->merge_beta, c0->merge_gamma,
+                              c0->stream));
   }
   // later work on the other contexts' streams must see the merged tables
   bool other = false;

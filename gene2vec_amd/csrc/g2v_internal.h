@@ -141,20 +141,23 @@ int sgns_blocks_per_cu(int K, int nv);
 hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
                                int64_t ld, int nvec, hipStream_t st);
 // replica merge (g2v_average*): rows of one [V][ld] table per call
-//   delta:  t <- t - old; cnt[row] = any(t - old != 0)
-//   apply:  touch: old <- old + t / max(cnt, 1)^beta; mean: old <- t * inv_n;  t <- old
-//   local:  the whole touch/mean merge over n replicas of one device
+//   delta:  t <- t - old; cnt[row] = any(t - old != 0); nsq[row] = |t - old|^2
+//   apply:  touch: old <- old + t / max(1, max(cnt, 1)^beta / gamma);
+//           align: old <- old + t / clamp(|t|^2 / nsq, 1, cnt);
+//           mean: old <- t * inv_n;  t <- old
+//   local:  the whole merge over n replicas of one device (D <= 512)
 constexpr int kMaxLocalReplicas = 16;
 struct LocalMergeArgs {
   float* t[kMaxLocalReplicas];
   float* old[kMaxLocalReplicas];
 };
-hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V, int64_t ld,
-                              int nvec, hipStream_t st);
-hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V, int64_t ld,
-                              int nvec, int rule, float inv_n, float beta, hipStream_t st);
+hipError_t launch_merge_delta(float* t, const float* old, float* cnt, float* nsq, int64_t V,
+                              int64_t ld, int nvec, hipStream_t st);
+hipError_t launch_merge_apply(float* t, float* old, const float* cnt, const float* nsq, int64_t V,
+                              int64_t ld, int nvec, int rule, float inv_n, float beta, float gamma,
+                              hipStream_t st);
 hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
-                              int rule, float beta, hipStream_t st);
+                              int rule, float beta, float gamma, hipStream_t st);
 // in-process replica group (g2v_comm_init_local): dst = sum over n sources,
 // added in source order from 0.f (k_merge_local's order)
 struct SumArgs {

@@ -359,11 +359,23 @@ hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
 // replica merge (g2v_average / g2v_average_local): one wave per row, lane l
 // owns float4 columns l, l+64; HBM-bound streaming (rows are 128-B aligned)
 // ---------------------------------------------------------------------------
+// every lane gets the wave's total (a fixed xor butterfly: the same bits on
+// every path that merges, so g2v_average_local and the all-reduce agree)
+__device__ __forceinline__ float wave_sum_f(float x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m);
+  return x;
+}
+
+__device__ __forceinline__ float sq4(float4 d) { return d.x * d.x + d.y * d.y + d.z * d.z + d.w * d.w; }
+
 // t <- t - old (the replica's change since the last merge, summed over ranks
-// by the all-reduce that follows), cnt[row] = 1 if the row changed
+// by the all-reduce that follows), cnt[row] = 1 if the row changed, nsq[row] =
+// |t - old|^2 (the align rule's denominator once summed over ranks)
 __global__ __launch_bounds__(256) void k_merge_delta(float* __restrict__ t,
                                                      const float* __restrict__ old,
-                                                     float* __restrict__ cnt, int64_t V,
+                                                     float* __restrict__ cnt,
+                                                     float* __restrict__ nsq, int64_t V,
                                                      int64_t ld, int nvec) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -371,38 +383,63 @@ __global__ __launch_bounds__(256) void k_merge_delta(float* __restrict__ t,
   float4* tr = reinterpret_cast<float4*>(t + r * ld);
   const float4* orw = reinterpret_cast<const float4*>(old + r * ld);
   int nz = 0;
+  float q = 0.f;
   for (int c = lane; c < nvec; c += 64) {
     const float4 x = tr[c], o = orw[c];
     const float4 d = make_float4(x.x - o.x, x.y - o.y, x.z - o.z, x.w - o.w);
     nz |= (d.x != 0.f) | (d.y != 0.f) | (d.z != 0.f) | (d.w != 0.f);
+    q += sq4(d);
     tr[c] = d;
   }
   const int any = __any(nz);
-  if (lane == 0) cnt[r] = any ? 1.f : 0.f;
+  q = wave_sum_f(q);
+  if (lane == 0) {
+    cnt[r] = any ? 1.f : 0.f;
+    nsq[r] = q;
+  }
 }
 
-// after the all-reduce: touch (rule 0) t holds sum_r d_r, cnt the number of
-// replicas that changed the row: new = old + t / max(cnt, 1)^beta (beta = 1:
-// the mean of the changes, 0: their sum); mean (rule 1) t holds sum_r t_r:
-// new = t * inv_n.  Both: old = t = new.
-__device__ __forceinline__ float touch_div(float k, float beta) {
-  return beta == 1.f ? k : powf(k, beta);
+// divisor of the summed change of a row k replicas changed:
+//   touch (rule 0): max(1, k^beta / gamma) (beta = gamma = 1: the mean; gamma
+//     scales the mean up, bounded by the sum; a row every replica drove to the
+//     same point moves gamma times that far)
+//   align (rule 2): |sum d|^2 / sum |d|^2 clamped to [1, k] -- k when the
+//     replicas' changes agree (a row they all drove to the same point: their
+//     mean), 1 when they are orthogonal (independent updates that one model
+//     would have applied all of: their sum)
+__device__ __forceinline__ float touch_div(float k, float beta, float gamma) {
+  const float kb = beta == 1.f ? k : powf(k, beta);
+  return gamma == 1.f ? kb : fmaxf(1.f, kb / gamma);
+}
+__device__ __forceinline__ float align_div(float k, float tsq, float nsq) {
+  return nsq > 0.f ? fminf(fmaxf(tsq / nsq, 1.f), fmaxf(k, 1.f)) : 1.f;
 }
 
+// after the all-reduce: touch / align: t holds sum_r d_r, cnt the number of
+// replicas that changed the row, nsq sum_r |d_r|^2: new = old + t / divisor;
+// mean (rule 1): t holds sum_r t_r: new = t * inv_n.  All: old = t = new.
 __global__ __launch_bounds__(256) void k_merge_apply(float* __restrict__ t, float* __restrict__ old,
-                                                     const float* __restrict__ cnt, int64_t V,
+                                                     const float* __restrict__ cnt,
+                                                     const float* __restrict__ nsq, int64_t V,
                                                      int64_t ld, int nvec, int rule, float inv_n,
-                                                     float beta) {
+                                                     float beta, float gamma) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= V) return;
   float4* tr = reinterpret_cast<float4*>(t + r * ld);
   float4* orw = reinterpret_cast<float4*>(old + r * ld);
-  const float k = rule == 0 ? touch_div(fmaxf(cnt[r], 1.f), beta) : 1.f;
+  float k = 1.f;
+  if (rule == 0) {
+    k = touch_div(fmaxf(cnt[r], 1.f), beta, gamma);
+  } else if (rule == 2) {
+    float q = 0.f;
+    for (int c = lane; c < nvec; c += 64) q += sq4(tr[c]);
+    k = align_div(cnt[r], wave_sum_f(q), nsq[r]);
+  }
   for (int c = lane; c < nvec; c += 64) {
     const float4 x = tr[c];
     float4 nv;
-    if (rule == 0) {
+    if (rule != 1) {
       const float4 o = orw[c];
       nv = make_float4(o.x + x.x / k, o.y + x.y / k, o.z + x.z / k, o.w + x.w / k);
     } else {
@@ -413,52 +450,71 @@ __global__ __launch_bounds__(256) void k_merge_apply(float* __restrict__ t, floa
   }
 }
 
-// n replicas on one device: the whole merge in one pass (deltas summed in
-// replica order)
+// n replicas on one device: the whole merge in one pass (deltas, counts and
+// squared norms summed in replica order, as the all-reduce path sums them);
+// a lane holds at most 2 float4 columns (D <= 512)
 __global__ __launch_bounds__(256) void k_merge_local(LocalMergeArgs a, int n, int64_t V,
-                                                     int64_t ld, int nvec, int rule, float beta) {
+                                                     int64_t ld, int nvec, int rule, float beta,
+                                                     float gamma) {
   const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (r >= V) return;
   const int64_t base = r * ld;
-  int k = 0;
-  if (rule == 0) {
-    for (int i = 0; i < n; ++i) {
-      const float4* tr = reinterpret_cast<const float4*>(a.t[i] + base);
-      const float4* orw = reinterpret_cast<const float4*>(a.old[i] + base);
-      int nz = 0;
-      for (int c = lane; c < nvec; c += 64) {
-        const float4 x = tr[c], o = orw[c];
-        nz |= (x.x - o.x != 0.f) | (x.y - o.y != 0.f) | (x.z - o.z != 0.f) | (x.w - o.w != 0.f);
+  float kc = 0.f, nq = 0.f;
+  float4 s[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+  for (int i = 0; i < n; ++i) {
+    const float4* tr = reinterpret_cast<const float4*>(a.t[i] + base);
+    const float4* orw = reinterpret_cast<const float4*>(a.old[i] + base);
+    int nz = 0;
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+      const int c = lane + 64 * v;
+      if (c >= nvec) continue;
+      const float4 x = tr[c];
+      if (rule != 1) {
+        const float4 o = orw[c];
+        const float4 d = make_float4(x.x - o.x, x.y - o.y, x.z - o.z, x.w - o.w);
+        nz |= (d.x != 0.f) | (d.y != 0.f) | (d.z != 0.f) | (d.w != 0.f);
+        q += sq4(d);
+        s[v].x += d.x;
+        s[v].y += d.y;
+        s[v].z += d.z;
+        s[v].w += d.w;
+      } else {
+        s[v].x += x.x;
+        s[v].y += x.y;
+        s[v].z += x.z;
+        s[v].w += x.w;
       }
-      k += __any(nz) ? 1 : 0;
+    }
+    if (rule != 1) {
+      kc += __any(nz) ? 1.f : 0.f;
+      nq += wave_sum_f(q);
     }
   }
-  const float kf = touch_div(k > 1 ? (float)k : 1.f, beta);
+  float kf = 1.f;
+  if (rule == 0) {
+    kf = touch_div(fmaxf(kc, 1.f), beta, gamma);
+  } else if (rule == 2) {
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < 2; ++v)
+      if (lane + 64 * v < nvec) q += sq4(s[v]);
+    kf = align_div(kc, wave_sum_f(q), nq);
+  }
   const float inv_n = 1.f / (float)n;
-  for (int c = lane; c < nvec; c += 64) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int i = 0; i < n; ++i) {
-      const float4 x = reinterpret_cast<const float4*>(a.t[i] + base)[c];
-      if (rule == 0) {
-        const float4 o = reinterpret_cast<const float4*>(a.old[i] + base)[c];
-        s.x += x.x - o.x;
-        s.y += x.y - o.y;
-        s.z += x.z - o.z;
-        s.w += x.w - o.w;
-      } else {
-        s.x += x.x;
-        s.y += x.y;
-        s.z += x.z;
-        s.w += x.w;
-      }
-    }
+#pragma unroll
+  for (int v = 0; v < 2; ++v) {
+    const int c = lane + 64 * v;
+    if (c >= nvec) continue;
     float4 nv;
-    if (rule == 0) {
+    if (rule != 1) {
       const float4 o = reinterpret_cast<const float4*>(a.old[0] + base)[c];
-      nv = make_float4(o.x + s.x / kf, o.y + s.y / kf, o.z + s.z / kf, o.w + s.w / kf);
+      nv = make_float4(o.x + s[v].x / kf, o.y + s[v].y / kf, o.z + s[v].z / kf,
+                       o.w + s[v].w / kf);
     } else {
-      nv = make_float4(s.x * inv_n, s.y * inv_n, s.z * inv_n, s.w * inv_n);
+      nv = make_float4(s[v].x * inv_n, s[v].y * inv_n, s[v].z * inv_n, s[v].w * inv_n);
     }
     for (int i = 0; i < n; ++i) {
       reinterpret_cast<float4*>(a.t[i] + base)[c] = nv;
@@ -511,27 +567,28 @@ hipError_t launch_sum_replicas(const SumArgs& a, int n, float* dst, int64_t coun
   return hipGetLastError();
 }
 
-hipError_t launch_merge_delta(float* t, const float* old, float* cnt, int64_t V, int64_t ld,
-                              int nvec, hipStream_t st) {
+hipError_t launch_merge_delta(float* t, const float* old, float* cnt, float* nsq, int64_t V,
+                              int64_t ld, int nvec, hipStream_t st) {
   if (V <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_merge_delta, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, old, cnt,
-                     V, ld, nvec);
+                     nsq, V, ld, nvec);
   return hipGetLastError();
 }
 
-hipError_t launch_merge_apply(float* t, float* old, const float* cnt, int64_t V, int64_t ld,
-                              int nvec, int rule, float inv_n, float beta, hipStream_t st) {
+hipError_t launch_merge_apply(float* t, float* old, const float* cnt, const float* nsq, int64_t V,
+                              int64_t ld, int nvec, int rule, float inv_n, float beta, float gamma,
+                              hipStream_t st) {
   if (V <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_merge_apply, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, old, cnt,
-                     V, ld, nvec, rule, inv_n, beta);
+                     nsq, V, ld, nvec, rule, inv_n, beta, gamma);
   return hipGetLastError();
 }
 
 hipError_t launch_merge_local(const LocalMergeArgs& a, int n, int64_t V, int64_t ld, int nvec,
-                              int rule, float beta, hipStream_t st) {
+                              int rule, float beta, float gamma, hipStream_t st) {
   if (V <= 0 || n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_merge_local, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, a, n, V, ld,
-                     nvec, rule, beta);
+                     nvec, rule, beta, gamma);
   return hipGetLastError();
 }
 

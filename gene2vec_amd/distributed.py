@@ -80,15 +80,17 @@ def average_(tensors, group=None):
         t.mul_(1.0 / world)
 
 
-def touch_merge_(tensors, olds, beta=1.0, group=None):
+def touch_merge_(tensors, olds, beta=1.0, group=None, align=False):
     """Row-wise replica merge: new = old + sum_r(d_r) / k**beta, d_r = replica r's
     change since the last merge, k = number of replicas whose row changed.
 
     A row only one replica trained keeps that replica's full update (plain
     averaging would divide it by N); a row every replica trained gets the
     mean of their updates (summing would overshoot the hot rows -- measured:
-    summed deltas diverge).  ``olds`` hold the tables at the last merge and
-    are updated in place."""
+    summed deltas diverge).  ``align``: libg2v's G2V_MERGE_ALIGN divisor
+    clamp(|sum_r d_r|^2 / sum_r |d_r|^2, 1, k) instead -- the mean of changes
+    that agree, the sum of independent ones.  ``olds`` hold the tables at the
+    last merge and are updated in place."""
     import torch
     import torch.distributed as dist
     single = not dist.is_initialized() or dist.get_world_size(group) == 1
@@ -97,12 +99,22 @@ def touch_merge_(tensors, olds, beta=1.0, group=None):
         # merges with one collective per quantity
         d = t - old
         cnt = (d != 0).any(dim=-1).to(t.dtype)
+        nsq = (d * d).sum(dim=-1) if align else None
         if not single:
             dist.all_reduce(d, op=dist.ReduceOp.SUM, group=group)
             dist.all_reduce(cnt, op=dist.ReduceOp.SUM, group=group)
-        k = torch.clamp(cnt, min=1.0)
-        if beta != 1.0:
-            k = k ** beta
+            if align:
+                dist.all_reduce(nsq, op=dist.ReduceOp.SUM, group=group)
+        if align:
+            tsq = (d * d).sum(dim=-1)
+            k = torch.where(nsq > 0, torch.minimum(torch.clamp(tsq / torch.clamp(nsq, min=1e-30),
+                                                               min=1.0),
+                                                   torch.clamp(cnt, min=1.0)),
+                            torch.ones_like(nsq))
+        else:
+            k = torch.clamp(cnt, min=1.0)
+            if beta != 1.0:
+                k = k ** beta
         d.div_(k.unsqueeze(-1))
         old.add_(d)
         t.copy_(old)
@@ -257,7 +269,7 @@ class ThreadAgreement:
         return agree
 
 
-MERGE_RULES = {"touch": 0, "mean": 1}  # == G2V_MERGE_TOUCH / G2V_MERGE_MEAN
+MERGE_RULES = {"touch": 0, "mean": 1, "align": 2}  # == G2V_MERGE_TOUCH / _MEAN / _ALIGN
 
 
 class ReplicaTrainer:
@@ -268,7 +280,8 @@ class ReplicaTrainer:
              and, for backend "libg2v", ``average(rule)`` (libg2v's g2v_average
              after g2v_comm_init / _init_host / _init_local).
     tables:  backend "torch" only: the torch tensors bound into the engine.
-    merge:   "touch" (row-wise, default) or "mean" (plain model averaging).
+    merge:   "touch" (row-wise, default), "align" (row-wise, agreement-scaled)
+             or "mean" (plain model averaging).
     backend: "libg2v" (merge inside libg2v, whatever its transport; "rccl" is
              an alias) or "torch" (torch.distributed).
     world:   ranks merging (default: the process group's size; an in-process
@@ -298,7 +311,7 @@ class ReplicaTrainer:
         # agree(int) -> min over ranks (window counts use the max, as -min(-x))
         self._agree = agree
         self.olds = ([t.clone() for t in self.tables]
-                     if merge == "touch" and backend == "torch" else None)
+                     if merge in ("touch", "align") and backend == "torch" else None)
         self.averages = 0
 
     def train_epoch(self, job_sent, alphas, seeds, timing=False, compute_loss=False):
@@ -360,8 +373,9 @@ class ReplicaTrainer:
     def sync_replicas(self):
         if self.backend == "libg2v":
             self.engine.average(MERGE_RULES[self.merge])
-        elif self.merge == "touch":
-            touch_merge_(self.tables, self.olds, self.beta, self.group)
+        elif self.merge in ("touch", "align"):
+            touch_merge_(self.tables, self.olds, self.beta, self.group,
+                         align=self.merge == "align")
         else:
             average_(self.tables, self.group)
         self.averages += 1

@@ -147,11 +147,14 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         call's last, shorter one -- with the replica merge
  *                         of g2v_average, on the same stream; every rank must
  *                         make the same number of merges (0 = off) [0]
- *   G2V_OPT_MERGE_RULE    rule of those merges, G2V_MERGE_TOUCH / _MEAN [TOUCH]
- *   G2V_OPT_MERGE_BETA_MILLI touch rule exponent x 1000: new = old + sum_r d_r /
- *                         k^beta (1000: the mean of the changes, 0: their sum);
- *                         used by g2v_average, the in-call merges and
- *                         g2v_average_local (the first context's) [1000]
+ *   G2V_OPT_MERGE_RULE    rule of those merges, G2V_MERGE_TOUCH / _MEAN / _ALIGN [TOUCH]
+ *   G2V_OPT_MERGE_BETA_MILLI, G2V_OPT_MERGE_GAMMA_MILLI  touch rule shape x 1000:
+ *                         new = old + sum_r d_r / max(1, k^beta / gamma)
+ *                         (beta = gamma = 1: the mean of the changes; beta 0:
+ *                         their sum; gamma > 1 scales the mean up, bounded by
+ *                         the sum); used by g2v_average, the in-call merges
+ *                         and g2v_average_local (the first context's)
+ *                         [1000, 1000]
  *   G2V_OPT_ACTIVE_WAVES  Hogwild kernel: waves per workgroup that train, 1..4;
  *                         with G2V_OPT_GRID 1 and 1 wave the production kernel
  *                         runs its chunks in record order, a deterministic
@@ -172,6 +175,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_STRIPE2_COPIES 14
 #define G2V_OPT_ACTIVE_WAVES 15
 #define G2V_OPT_MERGE_BETA_MILLI 16
+#define G2V_OPT_MERGE_GAMMA_MILLI 17
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
  * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest
@@ -274,10 +278,14 @@ int g2v_read_stats(g2v_ctx *ctx, g2v_stats *out);
 /* ---- multi-GPU replica averaging (no reference equivalent:
  * gensim is one process, src/gene2vec.py:59) ----------------------------------- */
 /* merge rules of g2v_average / g2v_average_local */
-#define G2V_MERGE_TOUCH 0 /* row-wise: new = old + sum_r(d_r) / k^beta, d_r = replica r's
-                             change since the last merge, k = replicas whose row changed,
-                             beta = G2V_OPT_MERGE_BETA_MILLI / 1000 */
+#define G2V_MERGE_TOUCH 0 /* row-wise: new = old + sum_r(d_r) / max(1, k^beta / gamma),
+                             d_r = replica r's change since the last merge, k = replicas
+                             whose row changed (G2V_OPT_MERGE_BETA/GAMMA_MILLI) */
 #define G2V_MERGE_MEAN 1  /* plain model averaging: new = sum_r(t_r) / nranks */
+#define G2V_MERGE_ALIGN 2 /* row-wise: new = old + sum_r(d_r) / clamp(|sum_r d_r|^2 /
+                             sum_r |d_r|^2, 1, k): the mean of changes that agree (a row
+                             every replica drove to the same point), the sum of
+                             independent ones (what one model would have applied) */
 /* rank 0 draws an RCCL unique id (128 bytes, ncclGetUniqueId) to hand to every
  * rank out of band (the Python driver broadcasts it over torch.distributed). */
 int g2v_comm_unique_id(void *id_out, int64_t id_bytes);

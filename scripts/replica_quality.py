@@ -99,9 +99,13 @@ def synthetic_gmt(path, pos, n_paths=300, max_genes=40, seed=0):
 def heldin(s0, s1, tok, counts, K, n=50000, seed=99):
     rng = np.random.Generator(np.random.PCG64(seed))
     idx = rng.integers(0, len(tok) // 2, n)
-    c, j = tok[2 * idx], tok[2 * idx + 1]
+    return objective(s0, s1, tok[2 * idx], tok[2 * idx + 1], counts, K, rng)
+
+
+def objective(s0, s1, c, j, counts, K, rng):
+    """mean SGNS objective of pairs (c, j) with K unigram^0.75 negatives"""
     p = counts.astype(np.float64) ** 0.75
-    negs = rng.choice(len(counts), size=(n, K), p=p / p.sum())
+    negs = rng.choice(len(counts), size=(len(c), K), p=p / p.sum())
     u = s0[j].astype(np.float64)
     pos = np.einsum("nd,nd->n", u, s1[c].astype(np.float64))
     neg = np.einsum("nd,nkd->nk", u, s1[negs].astype(np.float64))
@@ -109,6 +113,18 @@ def heldin(s0, s1, tok, counts, K, n=50000, seed=99):
 
 
 def export_and_score(tag, s0, index2word, counts, pos_genes, gmt, out, auc_seeds, D):
+    """exports (_w2v.txt, .txt) to a scratch directory, scored, then deleted
+    (tens of MB each: they stay out of gpurun_out)"""
+    import shutil
+    import tempfile
+    out = tempfile.mkdtemp(prefix="rq_")
+    try:
+        return _export_and_score(tag, s0, index2word, counts, pos_genes, gmt, out, auc_seeds, D)
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+def _export_and_score(tag, s0, index2word, counts, pos_genes, gmt, out, auc_seeds, D):
     from gene2vec_amd import evaluate as EV
     from gene2vec_amd import ggipnn as G
     from gene2vec_amd.word2vec import KeyedVectors, Vocab
@@ -136,8 +152,9 @@ def main():
     ap.add_argument("--pairs-per-replica", type=int, default=125_000_000)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--merge-every", default="1024", help="comma-separated job cadences")
-    ap.add_argument("--betas", default="1000",
-                    help="comma-separated touch-rule exponents x 1000 (G2V_OPT_MERGE_BETA_MILLI)")
+    ap.add_argument("--rules", default="1000:1000",
+                    help="comma-separated merge rules: 'align', 'mean', or a touch-rule shape "
+                         "beta:gamma x 1000 (G2V_OPT_MERGE_BETA_MILLI / _GAMMA_MILLI)")
     ap.add_argument("--no-eval", action="store_true",
                     help="held-in objective only (no exports, target function, GGIPNN)")
     ap.add_argument("--vocab", type=int, default=24447)
@@ -186,8 +203,19 @@ def main():
                          st.cuda_stream)
         st.synchronize()
 
+    # held-out pairs: a fresh draw of C3's Zipf generator (another seed), so
+    # memorising the training pairs does not count as quality
+    ho = S.zipf_gene_pairs(50000, a.vocab, 1.0, seed=777)
+    ho_c, ho_j = remap[ho[:, 0]], remap[ho[:, 1]]
+    keep = (ho_c >= 0) & (ho_j >= 0)
+    ho_c, ho_j = ho_c[keep], ho_j[keep]
+
+    def heldout(s0, s1):
+        return objective(s0, s1, ho_c, ho_j, vc, K, np.random.Generator(np.random.PCG64(98)))
+
     def finish(tag, s0, s1, extra):
-        res = {"heldin": round(heldin(s0, s1, tok, vc, K), 5)}
+        res = {"heldin": round(heldin(s0, s1, tok, vc, K), 5),
+               "heldout": round(heldout(s0, s1), 5)}
         if not a.no_eval:
             res.update(export_and_score(tag, s0, index2word, vc, pos_genes, gmt, a.out,
                                         [int(x) for x in a.auc_seeds.split(",")], D))
@@ -212,15 +240,21 @@ def main():
             eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)
             eng.sync()
             g0, g1 = eng.get_weights()
-            per_it.append(round(heldin(g0, g1, tok, vc, K, n=20000), 5))
+            per_it.append((round(heldin(g0, g1, tok, vc, K, n=20000), 5), round(heldout(g0, g1), 5)))
             print("single iter", it, per_it[-1], flush=True)
         s0, s1 = eng.get_weights()
         eng.close()
         finish("single", s0, s1, {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
 
     # ---- R replicas, libg2v merge every c jobs ---------------------------------------
-    combos = [(int(e), int(b)) for e in a.merge_every.split(",") for b in a.betas.split(",")]
-    for every, beta in combos:
+    def parse_rule(r):
+        if r in ("align", "mean"):
+            return r, 1000, 1000
+        b, g = r.split(":")
+        return "touch", int(b), int(g)
+    combos = [(int(e),) + parse_rule(r) for e in a.merge_every.split(",")
+              for r in a.rules.split(",")]
+    for every, rule, beta, gamma in combos:
         grp = E.LocalGroup(R)
         agree = Dd.ThreadAgreement(R)
         engs = []
@@ -229,11 +263,13 @@ def main():
             e.set_vocab(vc, a.sample)
             e.set_weights(syn0, np.zeros_like(syn0))
             e.set_option(N.OPT_MERGE_BETA_MILLI, beta)
+            e.set_option(N.OPT_MERGE_GAMMA_MILLI, gamma)
             engs.append(e)
         with ThreadPoolExecutor(max_workers=R) as ex:
             list(ex.map(lambda r: engs[r].comm_init_local(grp, r), range(R)))
-        trainers = [Dd.ReplicaTrainer(engs[r], (), every, N.MODE_HOGWILD, backend="libg2v",
-                                      world=R, agree=agree.for_rank(r)) for r in range(R)]
+        trainers = [Dd.ReplicaTrainer(engs[r], (), every, N.MODE_HOGWILD, merge=rule,
+                                      backend="libg2v", world=R, agree=agree.for_rank(r))
+                    for r in range(R)]
         rs = np.random.RandomState(1)  # model.random, identical on every rank
         t = time.time()
         per_it = []
@@ -255,15 +291,18 @@ def main():
             with ThreadPoolExecutor(max_workers=R) as ex:
                 list(ex.map(rank, range(R)))
             g0, g1 = engs[0].get_weights()
-            per_it.append(round(heldin(g0, g1, tok, vc, K, n=20000), 5))
-            print(f"replicas x{R} every {every} beta {beta} iter {it} {per_it[-1]}", flush=True)
+            per_it.append((round(heldin(g0, g1, tok, vc, K, n=20000), 5), round(heldout(g0, g1), 5)))
+            print(f"replicas x{R} every {every} {rule} beta {beta} gamma {gamma} iter {it} "
+                  f"{per_it[-1]}", flush=True)
         s0, s1 = engs[0].get_weights()
         same = all(np.array_equal(e.get_weights()[0], s0) for e in engs[1:])
         merges = trainers[0].averages
         for e in engs:
             e.close()
         grp.close()
-        finish(f"replicas{R}_every{every}" + (f"_beta{beta}" if beta != 1000 else ""), s0, s1,
+        finish(f"replicas{R}_every{every}" + (f"_{rule}" if rule != "touch" else "")
+               + (f"_beta{beta}" if beta != 1000 else "")
+               + (f"_gamma{gamma}" if gamma != 1000 else ""), s0, s1,
                {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it,
                 "merges_total": merges, "replicas_identical": same})
     if "single" in log["runs"]:
@@ -271,13 +310,15 @@ def main():
         for tag, r in log["runs"].items():
             if tag != "single":
                 r["heldin_gap"] = round((r["heldin"] - ref["heldin"]) / ref["heldin"], 5)
+                r["heldout_gap"] = round((r["heldout"] - ref["heldout"]) / ref["heldout"], 5)
                 if "auc_mean" in r and "auc_mean" in ref:
                     r["auc_gap"] = round((r["auc_mean"] - ref["auc_mean"]) / ref["auc_mean"], 5)
                     r["target_gap"] = round((r["target_ratio"] - ref["target_ratio"])
                                             / ref["target_ratio"], 5)
         json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
     for tag, r in log["runs"].items():
-        print(tag, {k: r[k] for k in ("heldin", "heldin_gap", "auc_mean", "auc_gap",
+        print(tag, {k: r[k] for k in ("heldin", "heldin_gap", "heldout", "heldout_gap",
+                                      "auc_mean", "auc_gap",
                                       "target_ratio", "target_gap") if k in r})
     print(json.dumps(log))
 

@@ -88,6 +88,16 @@ def _worker(rank, world, port, q):
         Dd.touch_merge_([t], olds)
         out["touch"] = t.numpy()
         out["touch_old"] = olds[0].numpy()
+        # align rule: row 0 both ranks move alike (agree: their mean), row 1
+        # orthogonally (independent: their sum), row 2 rank 1 only
+        t = torch.zeros(3, 2)
+        olds = [t.clone()]
+        t[0] = torch.tensor([1.0, 1.0])
+        t[1] = torch.tensor([1.0, 0.0]) if rank == 0 else torch.tensor([0.0, 2.0])
+        if rank == 1:
+            t[2] = torch.tensor([3.0, 0.0])
+        Dd.touch_merge_([t], olds, align=True)
+        out["align"] = t.numpy()
         # both tables in one [2][V][ld] buffer (bench.py's layout): same result
         # as merging each table on its own
         g = torch.Generator().manual_seed(rank)
@@ -198,6 +208,14 @@ def test_touch_merge_rowwise(results):
         assert np.allclose(t[2], 2.0)        # only rank 1
         assert np.allclose(t[3], 0.0)        # untouched
         assert np.array_equal(results[r]["touch_old"], t)
+
+
+def test_align_merge_rowwise(results):
+    for r in (0, 1):
+        a = results[r]["align"]
+        assert np.allclose(a[0], [1.0, 1.0])   # agreeing changes: their mean
+        assert np.allclose(a[1], [1.0, 2.0])   # orthogonal changes: their sum
+        assert np.allclose(a[2], [3.0, 0.0])   # one replica: its change
 
 
 def test_touch_merge_fused_buffer_equals_per_table(results):

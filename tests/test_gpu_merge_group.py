@@ -73,6 +73,19 @@ def _touch_ref(ts, olds):
     return olds[0] + s / np.maximum(k, np.float32(1))[:, None]
 
 
+def _align_ref(ts, olds):
+    """G2V_MERGE_ALIGN restated: new = old + s / clamp(|s|^2 / sum_r |d_r|^2, 1, k)"""
+    d = [t - o for t, o in zip(ts, olds)]
+    k = sum((x != 0).any(axis=1).astype(np.float32) for x in d)
+    s = np.zeros_like(d[0])
+    for x in d:
+        s = s + x
+    nsq = sum((x.astype(np.float64) ** 2).sum(1) for x in d)
+    tsq = (s.astype(np.float64) ** 2).sum(1)
+    div = np.where(nsq > 0, np.clip(tsq / np.maximum(nsq, 1e-300), 1, np.maximum(k, 1)), 1)
+    return olds[0] + s / div.astype(np.float32)[:, None]
+
+
 def _run_threads(fns):
     with ThreadPoolExecutor(max_workers=len(fns)) as ex:
         futs = [ex.submit(f) for f in fns]
@@ -80,7 +93,7 @@ def _run_threads(fns):
 
 
 @pytest.mark.parametrize("n", [2, 3, 5, 8])
-@pytest.mark.parametrize("rule", [N.MERGE_TOUCH, N.MERGE_MEAN])
+@pytest.mark.parametrize("rule", [N.MERGE_TOUCH, N.MERGE_MEAN, N.MERGE_ALIGN])
 def test_group_merge_equals_average_local_and_restatement(n, rule):
     """one window per replica, then g2v_average over the group: every rank
     holds g2v_average_local's tables bit for bit, which are the restated rule;
@@ -122,14 +135,18 @@ def test_group_merge_equals_average_local_and_restatement(n, rule):
             for tbl, init in ((0, syn0), (1, np.zeros_like(syn0))):
                 if rule == N.MERGE_TOUCH:
                     exp = _touch_ref([p[tbl] for p in pre], [init] * n)
+                elif rule == N.MERGE_ALIGN:
+                    exp = _align_ref([p[tbl] for p in pre], [init] * n)
                 else:
                     s = np.zeros_like(init)
                     for p in pre:
                         s = s + p[tbl]
                     exp = s * np.float32(1.0 / n)
-                np.testing.assert_allclose(ref[tbl], exp, rtol=1e-6, atol=1e-9)
+                # (align: the divisor's norms are summed in another order here)
+                np.testing.assert_allclose(ref[tbl], exp, rtol=1e-6 if rule != N.MERGE_ALIGN
+                                           else 1e-5, atol=1e-9)
                 # a row trained by one replica only keeps that replica's full update
-                if rule == N.MERGE_TOUCH and tbl == 1:
+                if rule != N.MERGE_MEAN and tbl == 1:
                     touched = [(p[1] != 0).any(axis=1) for p in pre]
                     only0 = touched[0] & ~np.any(touched[1:], axis=0)
                     if only0.any():
