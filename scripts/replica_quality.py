@@ -60,11 +60,47 @@ def positives():
     return out
 
 
-def build_corpus(R, per, V0, rep, seed):
+def module_of(V0, modules, seed=3):
+    """planted co-expression modules: gene g -> module (a random balanced split)"""
+    perm = np.random.RandomState(seed).permutation(V0)
+    mod = np.empty(V0, np.int64)
+    mod[perm] = np.arange(V0) % modules
+    return mod
+
+
+def planted_pairs(n, V0, mod, modules, p_in, shard):
+    """C3's Zipf(1) pairs, a fraction p_in of them rewired inside the first
+    gene's module (the second gene uniform among its module mates): every gene
+    keeps a Zipf-like degree and gains co-expression partners, so the target
+    function's pathways (= the modules) and its random pairs both mean something"""
+    pairs = S.zipf_gene_pairs(n, V0, 1.0, seed=20250114, shard=shard)
+    rng = np.random.Generator(np.random.PCG64(9000 + shard))
+    order = np.argsort(mod, kind="stable")
+    start = np.searchsorted(mod[order], np.arange(modules))
+    size = np.bincount(mod, minlength=modules)
+    sel = np.nonzero(rng.random(n) < p_in)[0]
+    a = pairs[sel, 0]
+    m = mod[a]
+    b = order[start[m] + (rng.random(len(sel)) * size[m]).astype(np.int64)]
+    bad = b == a
+    while bad.any():
+        mb = m[bad]
+        b[bad] = order[start[mb] + (rng.random(int(bad.sum())) * size[mb]).astype(np.int64)]
+        bad = b == a
+    pairs[sel, 1] = b
+    return pairs
+
+
+def build_corpus(R, per, V0, rep, seed, modules=0, p_in=0.0):
     """(pairs int32[N][2] in id space, names by id, positive pairs by name)"""
+    mod = module_of(V0, modules) if modules else None
+
+    def shard(r):
+        if modules:
+            return planted_pairs(per, V0, mod, modules, p_in, r)
+        return S.zipf_gene_pairs(per, V0, 1.0, seed=20250114, shard=r)
     with ThreadPoolExecutor(max_workers=min(R, 16)) as ex:
-        shards = list(ex.map(lambda r: S.zipf_gene_pairs(per, V0, 1.0, seed=20250114, shard=r),
-                             range(R)))
+        shards = list(ex.map(shard, range(R)))
     names = S.gene_names(V0)
     pos = positives()
     gid = {}
@@ -78,6 +114,15 @@ def build_corpus(R, per, V0, rep, seed):
     pairs = np.concatenate(parts)
     del shards, parts
     return pairs, names, pos
+
+
+def module_gmt(path, mod, modules, names, n_paths=300, seed=0):
+    """pathways = planted modules (random 300 of them)"""
+    rng = np.random.RandomState(seed)
+    with open(path, "w") as f:
+        for k, m in enumerate(rng.choice(modules, size=min(n_paths, modules), replace=False)):
+            genes = [names[g] for g in np.nonzero(mod == m)[0]]
+            f.write("\t".join([f"MODULE{m}", "http://synthetic"] + genes) + "\n")
 
 
 def synthetic_gmt(path, pos, n_paths=300, max_genes=40, seed=0):
@@ -162,6 +207,10 @@ def main():
     ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--sample", type=float, default=1e-3)
     ap.add_argument("--ggipnn-repeat", type=int, default=30)
+    ap.add_argument("--modules", type=int, default=0,
+                    help="plant this many co-expression modules in the Zipf pairs (the "
+                         "target function's pathways are then the modules)")
+    ap.add_argument("--p-module", type=float, default=0.5)
     ap.add_argument("--auc-seeds", default="0,1,2")
     ap.add_argument("--no-single", action="store_true")
     ap.add_argument("--out", default="gpurun_out/replica_quality")
@@ -170,7 +219,8 @@ def main():
     os.makedirs(a.out, exist_ok=True)
     R, D, K = a.replicas, a.dim, a.negative
     t0 = time.time()
-    pairs, names, pos = build_corpus(R, a.pairs_per_replica, a.vocab, a.ggipnn_repeat, 5)
+    pairs, names, pos = build_corpus(R, a.pairs_per_replica, a.vocab, a.ggipnn_repeat, 5,
+                                     a.modules, a.p_module)
     n = len(pairs)
     flat = pairs.reshape(-1)
     del pairs
@@ -183,7 +233,10 @@ def main():
     index2word = [names[i] for i in order]
     pos_genes = {g for p in pos for g in p}
     gmt = os.path.join(a.out, "synthetic.gmt")
-    synthetic_gmt(gmt, pos)
+    if a.modules:
+        module_gmt(gmt, module_of(a.vocab, a.modules), a.modules, names)
+    else:
+        synthetic_gmt(gmt, pos)
     seeds = np.array([zlib.crc32((w + "1").encode()) for w in index2word], np.uint32)
     syn0 = E.seeded_vectors(seeds, D)
     dev = torch.device("cuda", 0)
@@ -192,7 +245,8 @@ def main():
     rs_perm = np.random.RandomState(11)
     perm_seeds = [int(rs_perm.randint(0, 2 ** 62)) for _ in range(a.iters)]
     log = {"config": {"replicas": R, "pairs_per_replica": a.pairs_per_replica,
-                      "ggipnn_repeat": a.ggipnn_repeat, "pairs_total": n, "vocab": V,
+                      "ggipnn_repeat": a.ggipnn_repeat, "modules": a.modules,
+                      "p_module": a.p_module if a.modules else 0.0, "pairs_total": n, "vocab": V,
                       "dim": D, "negative": K, "sample": a.sample, "iters": a.iters},
            "corpus_s": round(time.time() - t0, 1), "runs": {}}
     print(json.dumps(log["config"]), flush=True)
