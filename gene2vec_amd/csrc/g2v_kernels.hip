@@ -406,7 +406,8 @@ __global__ __launch_bounds__(256) void k_merge_delta(float* __restrict__ t,
 //   align (rule 2): |sum d|^2 / sum |d|^2 clamped to [1, k] -- k when the
 //     replicas' changes agree (a row they all drove to the same point: their
 //     mean), 1 when they are orthogonal (independent updates that one model
-//     would have applied all of: their sum)
+//     would have applied all of: their sum) -- then shaped by beta / gamma
+//     like the touch divisor
 __device__ __forceinline__ float touch_div(float k, float beta, float gamma) {
   const float kb = beta == 1.f ? k : powf(k, beta);
   return gamma == 1.f ? kb : fmaxf(1.f, kb / gamma);
@@ -434,7 +435,7 @@ __global__ __launch_bounds__(256) void k_merge_apply(float* __restrict__ t, floa
   } else if (rule == 2) {
     float q = 0.f;
     for (int c = lane; c < nvec; c += 64) q += sq4(tr[c]);
-    k = align_div(cnt[r], wave_sum_f(q), nsq[r]);
+    k = touch_div(align_div(cnt[r], wave_sum_f(q), nsq[r]), beta, gamma);
   }
   for (int c = lane; c < nvec; c += 64) {
     const float4 x = tr[c];
@@ -501,7 +502,7 @@ __global__ __launch_bounds__(256) void k_merge_local(LocalMergeArgs a, int n, in
 #pragma unroll
     for (int v = 0; v < 2; ++v)
       if (lane + 64 * v < nvec) q += sq4(s[v]);
-    kf = align_div(kc, wave_sum_f(q), nq);
+    kf = touch_div(align_div(kc, wave_sum_f(q), nq), beta, gamma);
   }
   const float inv_n = 1.f / (float)n;
 #pragma unroll

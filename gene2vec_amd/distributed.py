@@ -80,17 +80,18 @@ def average_(tensors, group=None):
         t.mul_(1.0 / world)
 
 
-def touch_merge_(tensors, olds, beta=1.0, group=None, align=False):
+def touch_merge_(tensors, olds, beta=1.0, group=None, align=False, gamma=1.0):
     """Row-wise replica merge: new = old + sum_r(d_r) / k**beta, d_r = replica r's
     change since the last merge, k = number of replicas whose row changed.
 
     A row only one replica trained keeps that replica's full update (plain
     averaging would divide it by N); a row every replica trained gets the
     mean of their updates (summing would overshoot the hot rows -- measured:
-    summed deltas diverge).  ``align``: libg2v's G2V_MERGE_ALIGN divisor
-    clamp(|sum_r d_r|^2 / sum_r |d_r|^2, 1, k) instead -- the mean of changes
-    that agree, the sum of independent ones.  ``olds`` hold the tables at the
-    last merge and are updated in place."""
+    summed deltas diverge).  ``align``: libg2v's G2V_MERGE_ALIGN count
+    clamp(|sum_r d_r|^2 / sum_r |d_r|^2, 1, k) instead of k -- the mean of
+    changes that agree, the sum of independent ones; the divisor is then
+    max(1, count**beta / gamma).  ``olds`` hold the tables at the last merge
+    and are updated in place."""
     import torch
     import torch.distributed as dist
     single = not dist.is_initialized() or dist.get_world_size(group) == 1
@@ -113,8 +114,10 @@ def touch_merge_(tensors, olds, beta=1.0, group=None, align=False):
                             torch.ones_like(nsq))
         else:
             k = torch.clamp(cnt, min=1.0)
-            if beta != 1.0:
-                k = k ** beta
+        if beta != 1.0:
+            k = k ** beta
+        if gamma != 1.0:
+            k = torch.clamp(k / gamma, min=1.0)
         d.div_(k.unsqueeze(-1))
         old.add_(d)
         t.copy_(old)
@@ -294,7 +297,7 @@ class ReplicaTrainer:
     """
 
     def __init__(self, engine, tables=(), avg_every_jobs=1024, mode=0, merge="touch", beta=1.0,
-                 backend="torch", group=None, world=None, agree=None):
+                 backend="torch", group=None, world=None, agree=None, gamma=1.0):
         if backend == "rccl":
             backend = "libg2v"
         if backend not in ("torch", "libg2v"):
@@ -305,6 +308,7 @@ class ReplicaTrainer:
         self.mode = mode
         self.merge = merge
         self.beta = beta
+        self.gamma = gamma
         self.backend = backend
         self.group = group
         self._world = world
@@ -375,7 +379,7 @@ class ReplicaTrainer:
             self.engine.average(MERGE_RULES[self.merge])
         elif self.merge in ("touch", "align"):
             touch_merge_(self.tables, self.olds, self.beta, self.group,
-                         align=self.merge == "align")
+                         align=self.merge == "align", gamma=self.gamma)
         else:
             average_(self.tables, self.group)
         self.averages += 1

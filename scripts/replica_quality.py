@@ -302,10 +302,14 @@ def main():
 
     # ---- R replicas, libg2v merge every c jobs ---------------------------------------
     def parse_rule(r):
-        if r in ("align", "mean"):
-            return r, 1000, 1000
-        b, g = r.split(":")
-        return "touch", int(b), int(g)
+        """'mean', 'touch:B:G', 'align:B:G' (B, G = beta, gamma x 1000) or 'B:G' (touch)"""
+        parts = r.split(":")
+        if parts[0] in ("align", "mean", "touch"):
+            name, parts = parts[0], parts[1:]
+        else:
+            name = "touch"
+        b, g = (int(parts[0]), int(parts[1])) if parts else (1000, 1000)
+        return name, b, g
     combos = [(int(e),) + parse_rule(r) for e in a.merge_every.split(",")
               for r in a.rules.split(",")]
     for every, rule, beta, gamma in combos:
