@@ -213,6 +213,9 @@ def main():
     ap.add_argument("--p-module", type=float, default=0.5)
     ap.add_argument("--auc-seeds", default="0,1,2")
     ap.add_argument("--no-single", action="store_true")
+    ap.add_argument("--single-seeds", default="1",
+                    help="model.random seeds of the one-model runs (several: the one model's "
+                         "own run-to-run spread, the yardstick for the replica gaps)")
     ap.add_argument("--out", default="gpurun_out/replica_quality")
     a = ap.parse_args()
     import torch
@@ -279,11 +282,13 @@ def main():
         json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
 
     # ---- one model over the whole corpus ----------------------------------------
-    if not a.no_single:
+    for si, sseed in enumerate(int(x) for x in a.single_seeds.split(",")):
+        if a.no_single:
+            break
         eng = E.SGNSEngine(V, D, K)
         eng.set_vocab(vc, a.sample)
         eng.set_weights(syn0, np.zeros_like(syn0))
-        rs = np.random.RandomState(1)
+        rs = np.random.RandomState(sseed)
         js = E.plan_jobs(n_sent=n, sent_len=2)
         al = E.job_alphas(js, n)
         t = time.time()
@@ -295,10 +300,11 @@ def main():
             eng.sync()
             g0, g1 = eng.get_weights()
             per_it.append((round(heldin(g0, g1, tok, vc, K, n=20000), 5), round(heldout(g0, g1), 5)))
-            print("single iter", it, per_it[-1], flush=True)
+            print("single", sseed, "iter", it, per_it[-1], flush=True)
         s0, s1 = eng.get_weights()
         eng.close()
-        finish("single", s0, s1, {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
+        finish("single" if si == 0 else f"single_seed{sseed}", s0, s1,
+               {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
 
     # ---- R replicas, libg2v merge every c jobs ---------------------------------------
     def parse_rule(r):
@@ -366,7 +372,7 @@ def main():
     if "single" in log["runs"]:
         ref = log["runs"]["single"]
         for tag, r in log["runs"].items():
-            if tag != "single":
+            if tag != "single":  # gaps to the first one-model run
                 r["heldin_gap"] = round((r["heldin"] - ref["heldin"]) / ref["heldin"], 5)
                 r["heldout_gap"] = round((r["heldout"] - ref["heldout"]) / ref["heldout"], 5)
                 if "auc_mean" in r and "auc_mean" in ref:
