@@ -73,7 +73,8 @@ def parse():
     p.add_argument("--negative", type=int, default=5)
     p.add_argument("--sample", type=float, default=1e-3)
     p.add_argument("--zipf", type=float, default=1.0)
-    p.add_argument("--avg-every-jobs", type=int, default=1024, help="RCCL merge cadence (N>1)")
+    p.add_argument("--avg-every-jobs", type=int, default=4096,
+                   help="replica merge cadence in jobs per rank (N>1; the CLI's default)")
     p.add_argument("--merge", choices=("touch", "mean"), default="touch",
                    help="replica merge rule (gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")

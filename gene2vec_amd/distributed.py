@@ -296,7 +296,7 @@ class ReplicaTrainer:
     merges at all.
     """
 
-    def __init__(self, engine, tables=(), avg_every_jobs=1024, mode=0, merge="touch", beta=1.0,
+    def __init__(self, engine, tables=(), avg_every_jobs=4096, mode=0, merge="touch", beta=1.0,
                  backend="torch", group=None, world=None, agree=None, gamma=1.0):
         if backend == "rccl":
             backend = "libg2v"

@@ -232,8 +232,9 @@ def main(argv=None):
                         help="load every iteration's model back from the checkpoint just "
                              "written, as src/gene2vec.py:86 does (the kept in-memory model "
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
-    parser.add_argument("--merge-every-jobs", type=int, default=1024,
-                        help="data-parallel replica merge cadence (gensim jobs per rank)")
+    parser.add_argument("--merge-every-jobs", type=int, default=4096,
+                        help="data-parallel replica merge cadence (gensim jobs per rank; "
+                             "4096 = 7 merges per epoch at C3, DESIGN.md section 7a)")
     parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
                         default="auto",
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
