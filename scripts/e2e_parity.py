@@ -1,0 +1,194 @@
+"""End-to-end parity of the north-star metrics (verdict row n1):
+the GPU trainer vs the gensim restatement on the same input, through the
+reference's whole training flow.
+
+gensim 3.4 is absent, so "gensim" here is oracle/sgns_oracle.c's sequential
+trainer: gensim's workers=1 order (Appendix A), bit-compatible with the GPU's
+sequential mode and its sampled stream.  The GPU side is the production path
+(libg2v, k_sgns_atomic Hogwild).  Both train the reference's flow
+(src/gene2vec.py:67-92): 10 iterations, the pairs reshuffled before every
+iteration (one permutation per iteration, shared by both engines), the alpha
+sawtooth restarting at every train() call, per-job seeds from model.random,
+compute_loss on the last iteration.
+
+Corpus: Zipf(1) gene pairs over --vocab genes with --modules planted
+co-expression modules (scripts/replica_quality.planted_pairs: half the pairs
+rewired inside the first gene's module) plus the reference's GGIPNN positive
+pairs (data/predictionData, all three splits, label-leaky as in
+scripts/ggipnn_e2e.py) repeated --ggipnn-repeat times.
+
+Metrics after the 10th iteration:
+  loss     gensim's get_latest_training_loss() of the last train() call (the
+           GPU's Hogwild tally vs the oracle's terms summed in double; the
+           oracle's float32 running sum is reported as well)
+  heldin   SGNS objective on 50,000 corpus pairs
+  target   the manuscript target function (gene2vec_amd/evaluate.py) with the
+           planted modules as pathways
+  auc      GGIPNN test AUC (gene2vec_amd/ggipnn.py), mean over classifier seeds
+Each engine runs with --seeds model.random seeds (its own run-to-run spread).
+
+    python scripts/e2e_parity.py --out gpurun_out/e2e_parity
+"""
+import argparse
+import json
+import os
+import sys
+import time
+import zlib
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+import replica_quality as RQ  # noqa: E402
+from gene2vec_amd import _native as N  # noqa: E402
+from gene2vec_amd import engine as E  # noqa: E402
+from gene2vec_amd import synthetic as S  # noqa: E402
+from oracle import c_oracle as CO  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=4_000_000)
+    ap.add_argument("--vocab", type=int, default=5000)
+    ap.add_argument("--modules", type=int, default=200)
+    ap.add_argument("--p-module", type=float, default=0.5)
+    ap.add_argument("--ggipnn-repeat", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--dim", type=int, default=200)
+    ap.add_argument("--negative", type=int, default=5)
+    ap.add_argument("--sample", type=float, default=1e-3)
+    ap.add_argument("--seeds", default="1,2")
+    ap.add_argument("--auc-seeds", default="0,1,2")
+    ap.add_argument("--engines", default="gpu,oracle",
+                    help="gpu (libg2v Hogwild), gpu_seq (libg2v sequential mode), gpu_gridN "
+                         "(Hogwild on N workgroups), oracle (sequential), oracle_hogN (the C "
+                         "restatement's OpenMP Hogwild on N threads: gensim workers=N)")
+    ap.add_argument("--out", default="gpurun_out/e2e_parity")
+    a = ap.parse_args()
+    os.makedirs(a.out, exist_ok=True)
+    D, K = a.dim, a.negative
+    t0 = time.time()
+    mod = RQ.module_of(a.vocab, a.modules)
+    pairs = RQ.planted_pairs(a.pairs, a.vocab, mod, a.modules, a.p_module, 0)
+    names = S.gene_names(a.vocab)
+    pos = RQ.positives()
+    gid = {}
+    for x, y in pos:
+        for g in (x, y):
+            if g not in gid:
+                gid[g] = a.vocab + len(gid)
+    names += list(gid)
+    pp = np.array([[gid[x], gid[y]] for x, y in pos], np.int32)
+    pairs = np.concatenate([pairs] + [pp] * a.ggipnn_repeat)
+    n = len(pairs)
+    flat = pairs.reshape(-1)
+    counts, first = E.count_ids(flat, len(names))
+    order, remap = S.vocab_order(counts, first)
+    tok0 = remap[flat].astype(np.int32)
+    vc = counts[order].astype(np.int64)
+    V = len(order)
+    index2word = [names[i] for i in order]
+    pos_genes = {g for p in pos for g in p}
+    gmt = os.path.join(a.out, "modules.gmt")
+    RQ.module_gmt(gmt, mod, a.modules, names, n_paths=min(300, a.modules))
+    seeds_w = np.array([zlib.crc32((w + "1").encode()) for w in index2word], np.uint32)
+    syn0 = E.seeded_vectors(seeds_w, D)
+    # one permutation of the pairs per iteration, shared by both engines
+    # (src/gene2vec.py:52,80 reshuffle before every train() call)
+    rs_perm = np.random.RandomState(11)
+    perms = [rs_perm.permutation(n) for _ in range(a.iters)]
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    al = E.job_alphas(js, n)
+    off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
+    si, cum = CO.sample_int(vc, a.sample), CO.make_cum_table(vc)
+    lockf = np.ones(V, np.float32)
+    log = {"config": {"pairs_total": n, "vocab": V, "modules": a.modules,
+                      "ggipnn_repeat": a.ggipnn_repeat, "iters": a.iters, "dim": D,
+                      "negative": K, "sample": a.sample},
+           "corpus_s": round(time.time() - t0, 1), "runs": {}}
+    print(json.dumps(log["config"]), flush=True)
+
+    def tokens(it):
+        return np.ascontiguousarray(tok0.reshape(n, 2)[perms[it]].reshape(-1))
+
+    def train_gpu(seed, mode=N.MODE_HOGWILD, grid=0):
+        eng = E.SGNSEngine(V, D, K)
+        if grid:
+            eng.set_option(N.OPT_GRID, grid)
+        eng.set_vocab(vc, a.sample)
+        eng.set_weights(syn0, np.zeros_like(syn0))
+        rs = np.random.RandomState(seed)
+        for it in range(a.iters):
+            last = it == a.iters - 1
+            eng.set_corpus(tokens(it), sent_len=2)
+            if last:
+                eng.reset_loss()
+            eng.train(js, al, E.job_seeds(rs, len(js) - 1), mode, compute_loss=last)
+            eng.sync()
+        st = eng.read_stats()
+        extra = {"grid": int(eng.get_option(N.OPT_GRID))}
+        s0, s1 = eng.get_weights()
+        eng.close()
+        return s0, s1, {"loss": float(st["training_loss"]), **extra}
+
+    def train_oracle(seed, threads=0):
+        a0, a1 = syn0.copy(), np.zeros_like(syn0)
+        rs = np.random.RandomState(seed)
+        extra = {}
+        for it in range(a.iters):
+            last = it == a.iters - 1
+            loss = np.zeros(1, np.float32) if last and not threads else None
+            lex = np.zeros(1, np.float64) if last and not threads else None
+            CO.train(tokens(it), off, js, al.astype(np.float32), E.job_seeds(rs, len(js) - 1), si,
+                     a.sample != 0, cum, a0, a1, lockf, K, nthreads=threads, loss=loss,
+                     loss_exact=lex)
+            if last and not threads:
+                extra = {"loss": float(lex[0]), "loss_float32_running": float(loss[0])}
+            print(f"  oracle threads {threads} seed {seed} iteration {it + 1} done", flush=True)
+        return a0, a1, extra
+
+    for eng_name in a.engines.split(","):
+        for seed in (int(x) for x in a.seeds.split(",")):
+            t = time.time()
+            if eng_name == "gpu":
+                s0, s1, extra = train_gpu(seed)
+            elif eng_name == "gpu_seq":
+                s0, s1, extra = train_gpu(seed, N.MODE_SEQUENTIAL)
+            elif eng_name.startswith("gpu_grid"):
+                s0, s1, extra = train_gpu(seed, grid=int(eng_name[8:]))
+            elif eng_name.startswith("oracle_hog"):
+                s0, s1, extra = train_oracle(seed, int(eng_name[10:]))
+            else:
+                s0, s1, extra = train_oracle(seed)
+            tr = time.time() - t
+            res = {"train_s": round(tr, 1), **extra,
+                   "heldin": round(RQ.heldin(s0, s1, tok0, vc, K), 5)}
+            res.update(RQ.export_and_score(f"{eng_name}{seed}", s0, index2word, vc, pos_genes,
+                                           gmt, a.out,
+                                           [int(x) for x in a.auc_seeds.split(",") if x], D))
+            log["runs"][f"{eng_name}_seed{seed}"] = res
+            print(eng_name, seed, json.dumps(res), flush=True)
+            json.dump(log, open(os.path.join(a.out, "e2e_parity.json"), "w"), indent=1)
+
+    # gaps of the GPU runs to the oracle runs' mean, beside the oracle's own spread
+    def mean(engine, key):
+        v = [r[key] for t, r in log["runs"].items() if t.startswith(engine + "_seed") and key in r]
+        return float(np.mean(v)) if v else None
+    summ = {}
+    for key in ("loss", "heldin", "target_ratio", "auc_mean"):
+        g, o = mean("gpu", key), mean("oracle", key)
+        ov = [r[key] for t, r in log["runs"].items() if t.startswith("oracle_seed")]
+        summ[key] = {"gpu": g, "oracle": o,
+                     "gap": None if g is None or o is None else round((g - o) / o, 5),
+                     "oracle_spread": round((max(ov) - min(ov)) / abs(np.mean(ov)), 5)
+                     if len(ov) > 1 else None}
+    log["summary"] = summ
+    json.dump(log, open(os.path.join(a.out, "e2e_parity.json"), "w"), indent=1)
+    print(json.dumps(summ, indent=1))
+
+
+if __name__ == "__main__":
+    main()

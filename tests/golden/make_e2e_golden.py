@@ -1,0 +1,63 @@
+"""Golden values for tests/test_gpu_e2e_parity.py: the gensim restatement's
+(oracle/sgns_oracle.c, sequential = gensim workers=1 order) north-star metrics
+after the reference's 10-iteration flow on tests.helpers.e2e_corpus().
+
+    python tests/golden/make_e2e_golden.py     # ~2 minutes on one CPU
+
+Per model.random seed: the last iteration's training loss (gensim's
+compute_loss terms summed in double), the SGNS objective on 40,000 corpus
+pairs, and the manuscript target function (oracle/target_oracle.py, the
+planted modules as pathways).  Written to tests/golden/e2e_parity.json."""
+import json
+import os
+import sys
+import time
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from gene2vec_amd import engine as E  # noqa: E402
+from oracle import c_oracle as CO  # noqa: E402
+from oracle import target_oracle as TO  # noqa: E402
+from tests.helpers import E2E, e2e_corpus, e2e_heldin  # noqa: E402
+
+
+def main():
+    t0 = time.time()
+    tok, counts, index2word, lines, perms, wseeds = e2e_corpus()
+    n = len(tok) // 2
+    D, K, sample = E2E["D"], E2E["K"], E2E["sample"]
+    V = len(counts)
+    syn0 = E.seeded_vectors(wseeds, D)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    al = E.job_alphas(js, n).astype(np.float32)
+    off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
+    si, cum = CO.sample_int(counts, sample), CO.make_cum_table(counts)
+    out = {"config": dict(E2E, seeds=list(E2E["seeds"])),
+           "corpus_crc32": zlib.crc32(tok.tobytes()), "vocab": V, "runs": {}}
+    for seed in E2E["seeds"]:
+        a0, a1 = syn0.copy(), np.zeros_like(syn0)
+        rs = np.random.RandomState(seed)
+        for it in range(E2E["iters"]):
+            last = it == E2E["iters"] - 1
+            lex = np.zeros(1, np.float64) if last else None
+            tk = np.ascontiguousarray(tok.reshape(n, 2)[perms[it]].reshape(-1))
+            CO.train(tk, off, js, al, E.job_seeds(rs, len(js) - 1), si, sample != 0, cum, a0, a1,
+                     np.ones(V, np.float32), K, loss_exact=lex)
+        pm, rm, ratio = TO.target_function(index2word, a0, lines)
+        out["runs"][str(seed)] = {"loss": float(lex[0]),
+                                  "heldin": e2e_heldin(a0, a1, tok, counts, K),
+                                  "target_ratio": ratio, "path_mean": pm, "rand_mean": rm}
+        print(seed, out["runs"][str(seed)], f"{time.time() - t0:.0f} s", flush=True)
+    for key in ("loss", "heldin", "target_ratio"):
+        out[key + "_mean"] = float(np.mean([r[key] for r in out["runs"].values()]))
+    with open(os.path.join(HERE, "e2e_parity.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

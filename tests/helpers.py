@@ -111,3 +111,61 @@ def long_sentence_corpus(seed=0):
     tok = np.where(tok >= 0, remap[np.maximum(tok, 0)], -1).astype(np.int32)
     off = np.cumsum([0] + lengths).astype(np.int64)
     return tok, off, counts[order]
+
+
+# ---------------------------------------------------------------------------
+# end-to-end parity corpus (tests/test_gpu_e2e_parity.py,
+# tests/golden/make_e2e_golden.py): Zipf(1) pairs with planted co-expression
+# modules, the reference's 10-iteration flow, one permutation per iteration
+E2E = {"V0": 3000, "modules": 100, "p_in": 0.5, "pairs": 2_000_000, "iters": 10, "D": 200,
+       "K": 5, "sample": 1e-3, "seeds": (1, 2, 3)}
+
+
+def e2e_corpus():
+    """(tok int32[2n] in vocab index order, vocab counts, index2word, pathway
+    lines (gmt text, newline kept as the reference reads them), per-iteration
+    permutations, seeded syn0)"""
+    c = E2E
+    V0, M = c["V0"], c["modules"]
+    pairs = zipf_pairs(c["pairs"], V0, 1.0, seed=20250114)
+    mod = np.empty(V0, np.int64)
+    mod[np.random.RandomState(3).permutation(V0)] = np.arange(V0) % M
+    rng = np.random.Generator(np.random.PCG64(9000))
+    order_m = np.argsort(mod, kind="stable")
+    start = np.searchsorted(mod[order_m], np.arange(M))
+    size = np.bincount(mod, minlength=M)
+    sel = np.nonzero(rng.random(len(pairs)) < c["p_in"])[0]
+    a = pairs[sel, 0]
+    m = mod[a]
+    b = order_m[start[m] + (rng.random(len(sel)) * size[m]).astype(np.int64)]
+    bad = b == a
+    while bad.any():
+        b[bad] = order_m[start[m[bad]] + (rng.random(int(bad.sum())) * size[m[bad]]).astype(np.int64)]
+        bad = b == a
+    pairs[sel, 1] = b
+    order, remap, counts = vocab_from_ids(pairs.reshape(-1), V0)
+    tok = remap[pairs.reshape(-1)].astype(np.int32)
+    names = [f"G{i:05d}" for i in range(V0)]
+    index2word = [names[i] for i in order]
+    lines = []
+    for k in range(M):
+        genes = [names[g] for g in np.nonzero(mod == k)[0]]
+        lines.append("\t".join([f"MODULE{k}", "http://synthetic"] + genes) + "\n")
+    n = len(pairs)
+    rs = np.random.RandomState(11)
+    perms = [rs.permutation(n) for _ in range(c["iters"])]
+    seeds = np.array([crc_hash(w + "1") for w in index2word], np.uint32)
+    return tok, counts, index2word, lines, perms, seeds
+
+
+def e2e_heldin(s0, s1, tok, counts, K, n=40000, seed=99):
+    """SGNS objective on n corpus pairs with K unigram^0.75 negatives"""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    idx = rng.integers(0, len(tok) // 2, n)
+    c, j = tok[2 * idx], tok[2 * idx + 1]
+    p = counts.astype(np.float64) ** 0.75
+    negs = rng.choice(len(counts), size=(n, K), p=p / p.sum())
+    u = s0[j].astype(np.float64)
+    pos = np.einsum("nd,nd->n", u, s1[c].astype(np.float64))
+    neg = np.einsum("nd,nkd->nk", u, s1[negs].astype(np.float64))
+    return float((np.logaddexp(0, -pos) + np.logaddexp(0, neg).sum(1)).mean())

@@ -1,0 +1,77 @@
+"""GPU: the north-star metrics end to end (SURVEY.md 8(c) "final-epoch loss,
+target function ... within a stated tolerance of gensim on the same input").
+
+gensim is absent, so its stand-in is oracle/sgns_oracle.c's sequential
+trainer (gensim workers=1 order), whose results on this corpus are committed
+in tests/golden/e2e_parity.json (tests/golden/make_e2e_golden.py).  The GPU
+runs the production path -- libg2v's Hogwild kernel at the default grid --
+through the reference's flow (src/gene2vec.py:67-92): 10 iterations, the
+pairs reshuffled before each (the same permutations as the golden run), the
+alpha sawtooth restarting per train() call, compute_loss on the last one.
+Means over the same three model.random seeds; bars 1 % (north star) for the
+final-iteration loss and the manuscript target function
+(src/evaluation_target_function.py, planted modules as pathways) and 0.5 %
+for the SGNS objective on corpus pairs.  The Hogwild staleness shows in the
+target function most (-0.7 % here, -1.4 % on a denser
+10 k-gene corpus, -0.25 % at the C2 vocabulary; gensim's own 32-thread
+Hogwild, restated, sits 0.1-0.8 % below its sequential order)."""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from gene2vec_amd import _native as N
+from gene2vec_amd import engine as E
+from gene2vec_amd import evaluate as EV
+from gene2vec_amd.word2vec import KeyedVectors, Vocab
+from tests.conftest import GOLDEN
+from tests.helpers import E2E, e2e_corpus, e2e_heldin
+
+pytestmark = pytest.mark.gpu
+
+
+def test_gpu_hogwild_end_to_end_metrics_within_one_percent_of_sequential(tmp_path):
+    with open(os.path.join(GOLDEN, "e2e_parity.json")) as f:
+        ref = json.load(f)
+    tok, counts, index2word, lines, perms, wseeds = e2e_corpus()
+    assert zlib.crc32(tok.tobytes()) == ref["corpus_crc32"]
+    n = len(tok) // 2
+    D, K, sample = E2E["D"], E2E["K"], E2E["sample"]
+    V = len(counts)
+    syn0 = E.seeded_vectors(wseeds, D)
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    al = E.job_alphas(js, n)
+    got = {"loss": [], "heldin": [], "target_ratio": []}
+    for seed in E2E["seeds"]:
+        eng = E.SGNSEngine(V, D, K)
+        eng.set_vocab(counts, sample)
+        eng.set_weights(syn0, np.zeros_like(syn0))
+        rs = np.random.RandomState(seed)
+        for it in range(E2E["iters"]):
+            last = it == E2E["iters"] - 1
+            eng.set_corpus(np.ascontiguousarray(tok.reshape(n, 2)[perms[it]].reshape(-1)),
+                           sent_len=2)
+            if last:
+                eng.reset_loss()
+            eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD, compute_loss=last)
+        eng.sync()
+        loss = eng.read_stats()["training_loss"]
+        s0, s1 = eng.get_weights()
+        eng.close()
+        kv = KeyedVectors(D)
+        kv.index2word = list(index2word)
+        kv.vocab = {w: Vocab(count=int(counts[i]), index=i) for i, w in enumerate(index2word)}
+        kv.vectors = np.ascontiguousarray(s0)
+        w2v = str(tmp_path / f"seed{seed}_w2v.txt")
+        kv.save_word2vec_format(w2v)
+        t = EV.target_function(w2v, pathways=lines, strict=False, verbose=False)
+        got["loss"].append(float(loss))
+        got["heldin"].append(e2e_heldin(s0, s1, tok, counts, K))
+        got["target_ratio"].append(float(t["ratio"]))
+    gaps = {k: (np.mean(v) - ref[k + "_mean"]) / ref[k + "_mean"] for k, v in got.items()}
+    print("gpu", got, "gaps vs sequential oracle", gaps)
+    assert abs(gaps["loss"]) < 0.01, gaps
+    assert abs(gaps["heldin"]) < 0.005, gaps
+    assert abs(gaps["target_ratio"]) < 0.01, gaps
