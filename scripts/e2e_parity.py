@@ -114,10 +114,12 @@ def main():
     def tokens(it):
         return np.ascontiguousarray(tok0.reshape(n, 2)[perms[it]].reshape(-1))
 
-    def train_gpu(seed, mode=N.MODE_HOGWILD, grid=0):
+    def train_gpu(seed, mode=N.MODE_HOGWILD, grid=0, overlap=None):
         eng = E.SGNSEngine(V, D, K)
         if grid:
             eng.set_option(N.OPT_GRID, grid)
+        if overlap is not None:
+            eng.set_option(N.OPT_ATOMIC_OVERLAP, overlap)
         eng.set_vocab(vc, a.sample)
         eng.set_weights(syn0, np.zeros_like(syn0))
         rs = np.random.RandomState(seed)
@@ -157,6 +159,8 @@ def main():
                 s0, s1, extra = train_gpu(seed)
             elif eng_name == "gpu_seq":
                 s0, s1, extra = train_gpu(seed, N.MODE_SEQUENTIAL)
+            elif eng_name.startswith("gpu_ov"):
+                s0, s1, extra = train_gpu(seed, overlap=int(eng_name[6:]))
             elif eng_name.startswith("gpu_grid"):
                 s0, s1, extra = train_gpu(seed, grid=int(eng_name[8:]))
             elif eng_name.startswith("oracle_hog"):
