@@ -28,6 +28,11 @@
 
 using namespace g2v;
 
+namespace g2v {
+hipError_t launch_row_norm2_max(const float* t, int V, int64_t ld, int D, unsigned int* out,
+                                hipStream_t st);  // g2v_kernels.hip
+}
+
 namespace {
 
 thread_local std::string g_err;
@@ -133,6 +138,8 @@ struct g2v_ctx {
   int cus = 0, sgns_grid = 0;
   bool grid_user = false;       // G2V_OPT_GRID set explicitly
   double u_max = 0.0;           // hottest row's updates per example (set_vocab)
+  double p_tok_max = 0.0;       // hottest row's share of the kept tokens (syn0 input rate)
+  int call_grid = 0;            // this g2v_train call's Hogwild grid (0: sgns_grid)
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
@@ -212,6 +219,7 @@ struct g2v_ctx {
   float* log_table = nullptr;
   double* d_loss = nullptr;
   unsigned int* d_queue = nullptr;  // k_sgns_atomic work queue (one counter)
+  unsigned int* d_norm = nullptr;   // stability_grid's max squared row norm (float bits)
 
   // replica merge: snapshot of both tables at the last merge, touched-row counts
   float *merge0 = nullptr, *merge1 = nullptr, *merge_cnt = nullptr;
@@ -259,9 +267,13 @@ constexpr double kStaleBudget = 125.0;
 // (C2 266 WGs: 202.6 M ex/s vs 197.2 with 8); below, the grid is held down by
 // the staleness budget, per-example latency binds and 8 win (C2 sample 0 at
 // 162 WGs: 153.6 vs 136.4; C4 at 121: 36.8 vs 36.1).
+// the Hogwild grid of the launches being issued: the call's stability cap
+// (train_impl) or the context's grid
+static int launch_grid(const g2v_ctx* c) { return c->call_grid > 0 ? c->call_grid : c->sgns_grid; }
+
 static int stripe_copies_eff(const g2v_ctx* c) {
   if (c->stripe_copies > 0) return c->stripe_copies;
-  return c->sgns_grid >= c->cus ? 16 : 8;
+  return launch_grid(c) >= c->cus ? 16 : 8;
 }
 
 // Second stripe tier when G2V_OPT_STRIPE2_ROWS is not set: rows 8..19 get 4
@@ -271,7 +283,7 @@ static int stripe_copies_eff(const g2v_ctx* c) {
 // vs 157.0; C4 at 121: 36.6 vs 36.7)
 static int stripe2_rows_eff(const g2v_ctx* c) {
   if (c->stripe2_rows >= 0) return c->stripe2_rows;
-  return c->sgns_grid >= c->cus ? 20 : 0;
+  return launch_grid(c) >= c->cus ? 20 : 0;
 }
 
 static int default_grid(int cus, int K, int nv, double u_max) {
@@ -456,7 +468,8 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
       (rc = dev_alloc(&c->bkt, (size_t)kBuckets + 1)) ||
       (rc = dev_alloc(&c->d_counts, (size_t)c->V)) || (rc = dev_alloc(&c->d_cpow, (size_t)c->V)) ||
       (rc = dev_alloc(&c->d_counters, 4)) || (rc = dev_alloc(&c->log_table, kExpTableSize)) ||
-      (rc = dev_alloc(&c->d_loss, 2)) || (rc = dev_alloc(&c->d_queue, 1)))
+      (rc = dev_alloc(&c->d_loss, 2)) || (rc = dev_alloc(&c->d_queue, 1)) ||
+      (rc = dev_alloc(&c->d_norm, 1)))
     return bail(rc);
   c->syn0 = c->own0;
   c->syn1 = c->own1;
@@ -526,6 +539,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->log_table);
   dev_free(c->d_loss);
   dev_free(c->d_queue);
+  dev_free(c->d_norm);
   dev_free(c->merge0);
   dev_free(c->merge1);
   dev_free(c->merge_cnt);
@@ -711,9 +725,13 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
       pt[i] = v * std::min(1.0, (sqrt(v / thr) + 1.0) * (thr / v));
       zt += pt[i];
     }
-    double um = 0.0;
-    for (int32_t i = 0; i < c->V; ++i) um = std::max(um, c->K * pn[i] / zn + pt[i] / zt);
+    double um = 0.0, pm = 0.0;
+    for (int32_t i = 0; i < c->V; ++i) {
+      um = std::max(um, c->K * pn[i] / zn + pt[i] / zt);
+      pm = std::max(pm, pt[i] / zt);
+    }
     c->u_max = um;
+    c->p_tok_max = pm;
     if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
   }
   HIPCHK(hipMemcpyAsync(c->d_counts, counts, sizeof(int64_t) * c->V, hipMemcpyHostToDevice,
@@ -1073,7 +1091,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     if ((rc = ctx_event(c, &e0)) || (rc = ctx_event(c, &e1))) return rc;
     HIPCHK(hipEventRecord(e0, c->stream));
   }
-  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, c->sgns_grid, c->stream));
+  HIPCHK(launch_sgns(s, c->K, c->nv, mode, c->cache_policy, launch_grid(c), c->stream));
   HIPCHK(launch_fold_stripes(c->syn0, c->syn1, c->stripe, s.stripe_rows, s.stripe_copies, c->ld,
                              c->nvec, c->stream));
   if (tier2)
@@ -1086,7 +1104,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     c->t_sgns.emplace_back(e0, e1);
   }
   if (atomic_kernel) {
-    c->last_grid = c->sgns_grid;
+    c->last_grid = launch_grid(c);
     c->last_stripe_rows = s.stripe_rows;
     c->last_stripe_copies = s.stripe_copies;
     c->last_stripe2_rows = s.stripe2_rows;
@@ -1182,6 +1200,42 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
 
 }  // extern "C"
 
+// Stability cap of the Hogwild grid for one g2v_train call.  The staleness
+// budget of default_grid bounds the in-flight updates of the hottest syn1neg
+// row; a hot syn0 row is the other risk: its delta sums K+1 terms g * syn1neg[t],
+// so in-flight updates to it overshoot once waves x p_tok x (K+1) x alpha x
+// |syn1neg|^2 grows, which it does as training structures the vectors.
+// Measured, with |syn1neg|^2 the largest squared row norm of
+// syn1neg (a hot input's centres are any rows): a 3,000-gene corpus with
+// planted modules at sample 0 diverged at a later sawtooth restart with 163
+// and 137 workgroups (a hot syn0 row's |v|^2 jumping 14 -> 90-215 and frozen
+// there by the |f| >= 6 skip; products 190-250) and trained to the
+// sequential order's objective at 64 (product 90); the other corpora measured
+// (C2 / C4 vocabularies, sample 1e-3, and pure Zipf at sample 0) stay below
+// the cap at their default grids.  So the call's grid is capped where the
+// product, from |syn1neg|^2 at the call's start and the call's largest alpha,
+// reaches 100.
+constexpr double kSyn0Budget = 100.0;
+
+static int stability_grid(g2v_ctx* c, const float* job_alpha, int64_t n_jobs) {
+  double amax = 0.0;
+  for (int64_t j = 0; j < n_jobs; ++j) amax = std::max(amax, (double)job_alpha[j]);
+  unsigned int bits = 0;
+  HIPCHK(hipMemsetAsync(c->d_norm, 0, sizeof(unsigned int), c->stream));
+  HIPCHK(launch_row_norm2_max(c->syn1, c->V, c->ld, c->D, c->d_norm, c->stream));
+  HIPCHK(hipMemcpyAsync(&bits, c->d_norm, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  float k1f;
+  memcpy(&k1f, &bits, sizeof k1f);
+  const double k1 = (double)k1f;
+  const double per_wave = c->p_tok_max * (c->K + 1) * amax * k1;
+  if (per_wave <= 0.0) return G2V_OK;
+  const double waves = kSyn0Budget / per_wave;
+  const int cap = (int)std::max(1.0, std::floor(waves / c->active_waves));
+  if (cap < c->sgns_grid) c->call_grid = cap;
+  return G2V_OK;
+}
+
 static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha,
                       const uint64_t* job_seed, int64_t n_jobs, uint32_t flags) {
   int rc;
@@ -1195,6 +1249,13 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
   if (n_jobs == 0) return G2V_OK;
   const bool timing = flags & G2V_FLAG_TIMING;
   const bool closs = flags & G2V_FLAG_COMPUTE_LOSS;
+  c->call_grid = 0;
+  if (mode == kModeHogwild && !c->grid_user && (rc = stability_grid(c, job_alpha, n_jobs)))
+    return rc;
+  struct ResetCallGrid {
+    g2v_ctx* c;
+    ~ResetCallGrid() { c->call_grid = 0; }
+  } reset_call_grid{c};
   if ((rc = upload_jobs(c, job_sent, job_alpha, job_seed, n_jobs))) return rc;
   // segments of <= seg_jobs jobs; with G2V_OPT_MERGE_EVERY_JOBS and a
   // communicator, windows of merge_every jobs end with a replica merge

@@ -347,6 +347,28 @@ __global__ void k_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
   *m = acc;
 }
 
+// largest squared row norm of a [V][ld] table (the Hogwild stability cap of
+// g2v_train): one wave per row, the float bits of a non-negative sum ordered
+// like unsigned integers, so one atomicMax keeps the maximum
+__global__ void k_row_norm2_max(const float* t, int V, int64_t ld, int D, unsigned int* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= V) return;
+  const float* row = t + r * ld;
+  float s = 0.f;
+  for (int i = lane; i < D; i += 64) s = fmaf(row[i], row[i], s);
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) atomicMax(out, __float_as_uint(s));
+}
+
+hipError_t launch_row_norm2_max(const float* t, int V, int64_t ld, int D, unsigned int* out,
+                                hipStream_t st) {
+  if (V <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_row_norm2_max, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, V, ld, D,
+                     out);
+  return hipGetLastError();
+}
+
 hipError_t launch_fold_stripes(float* syn0, float* syn1, float* stripe, int rows, int copies,
                                int64_t ld, int nvec, hipStream_t st) {
   if (rows <= 0 || copies <= 1) return hipSuccess;

@@ -115,8 +115,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_SEG_JOBS      gensim jobs per sampling/update segment [1024]
  *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = the staleness-bounded
  *                         default, RECOMPUTED by every g2v_set_vocab from the
- *                         vocabulary (g2v_get_option reads the value in use;
- *                         g2v_stats reports the last launch's) [0]
+ *                         vocabulary, and lowered for a Hogwild g2v_train call
+ *                         whose hot syn0 rows would overshoot (the call's
+ *                         largest alpha and |syn1neg|^2)
+ *                         (g2v_get_option reads set_vocab's value; g2v_stats
+ *                         reports the last launch's); > 0 = fixed, no cap [0]
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
  *                         2 uncached (re-allocates, zero-filled) [0]
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of

@@ -66,6 +66,7 @@ def main():
                     help="gpu (libg2v Hogwild), gpu_seq (libg2v sequential mode), gpu_gridN "
                          "(Hogwild on N workgroups), oracle (sequential), oracle_hogN (the C "
                          "restatement's OpenMP Hogwild on N threads: gensim workers=N)")
+    ap.add_argument("--per-iter", action="store_true", help="print the GPU runs' objective per iteration")
     ap.add_argument("--out", default="gpurun_out/e2e_parity")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
@@ -130,8 +131,17 @@ def main():
                 eng.reset_loss()
             eng.train(js, al, E.job_seeds(rs, len(js) - 1), mode, compute_loss=last)
             eng.sync()
+            if a.per_iter:
+                g0, g1 = eng.get_weights()
+                n0 = (g0.astype(np.float64) ** 2).sum(1)
+                n1 = (g1.astype(np.float64) ** 2).sum(1)
+                print(f"  gpu grid {grid} (call {eng.read_stats()['sgns_grid']}) seed {seed} "
+                      f"iteration {it + 1} heldin "
+                      f"{RQ.heldin(g0, g1, tok0, vc, K, n=20000):.5f} |syn0|^2 max/top20 "
+                      f"{n0.max():.2f}/{n0[:20].max():.2f} |syn1neg|^2 max/top20 "
+                      f"{n1.max():.2f}/{n1[:20].max():.2f}", flush=True)
         st = eng.read_stats()
-        extra = {"grid": int(eng.get_option(N.OPT_GRID))}
+        extra = {"grid": int(eng.get_option(N.OPT_GRID)), "last_call_grid": int(st["sgns_grid"])}
         s0, s1 = eng.get_weights()
         eng.close()
         return s0, s1, {"loss": float(st["training_loss"]), **extra}

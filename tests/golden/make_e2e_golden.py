@@ -36,25 +36,35 @@ def main():
     js = E.plan_jobs(n_sent=n, sent_len=2)
     al = E.job_alphas(js, n).astype(np.float32)
     off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
-    si, cum = CO.sample_int(counts, sample), CO.make_cum_table(counts)
+    cum = CO.make_cum_table(counts)
     out = {"config": dict(E2E, seeds=list(E2E["seeds"])),
            "corpus_crc32": zlib.crc32(tok.tobytes()), "vocab": V, "runs": {}}
-    for seed in E2E["seeds"]:
-        a0, a1 = syn0.copy(), np.zeros_like(syn0)
-        rs = np.random.RandomState(seed)
-        for it in range(E2E["iters"]):
-            last = it == E2E["iters"] - 1
-            lex = np.zeros(1, np.float64) if last else None
-            tk = np.ascontiguousarray(tok.reshape(n, 2)[perms[it]].reshape(-1))
-            CO.train(tk, off, js, al, E.job_seeds(rs, len(js) - 1), si, sample != 0, cum, a0, a1,
-                     np.ones(V, np.float32), K, loss_exact=lex)
-        pm, rm, ratio = TO.target_function(index2word, a0, lines)
-        out["runs"][str(seed)] = {"loss": float(lex[0]),
-                                  "heldin": e2e_heldin(a0, a1, tok, counts, K),
-                                  "target_ratio": ratio, "path_mean": pm, "rand_mean": rm}
-        print(seed, out["runs"][str(seed)], f"{time.time() - t0:.0f} s", flush=True)
+    def runs(smp):
+        si = CO.sample_int(counts, smp)
+        res = {}
+        for seed in E2E["seeds"]:
+            a0, a1 = syn0.copy(), np.zeros_like(syn0)
+            rs = np.random.RandomState(seed)
+            for it in range(E2E["iters"]):
+                last = it == E2E["iters"] - 1
+                lex = np.zeros(1, np.float64) if last else None
+                tk = np.ascontiguousarray(tok.reshape(n, 2)[perms[it]].reshape(-1))
+                CO.train(tk, off, js, al, E.job_seeds(rs, len(js) - 1), si, smp != 0, cum, a0,
+                         a1, np.ones(V, np.float32), K, loss_exact=lex)
+            pm, rm, ratio = TO.target_function(index2word, a0, lines)
+            res[str(seed)] = {"loss": float(lex[0]), "heldin": e2e_heldin(a0, a1, tok, counts, K),
+                              "target_ratio": ratio, "path_mean": pm, "rand_mean": rm}
+            print(smp, seed, res[str(seed)], f"{time.time() - t0:.0f} s", flush=True)
+        return res
+    out["runs"] = runs(sample)
     for key in ("loss", "heldin", "target_ratio"):
         out[key + "_mean"] = float(np.mean([r[key] for r in out["runs"].values()]))
+    # sample = 0 (no downsampling): the hot rows' staleness case of
+    # g2v_train's stability cap (g2v_api.hip stability_grid)
+    s0 = {"runs": runs(0.0)}
+    for key in ("loss", "heldin", "target_ratio"):
+        s0[key + "_mean"] = float(np.mean([r[key] for r in s0["runs"].values()]))
+    out["sample0"] = s0
     with open(os.path.join(HERE, "e2e_parity.json"), "w") as f:
         json.dump(out, f, indent=1)
 

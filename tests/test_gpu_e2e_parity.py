@@ -32,20 +32,21 @@ from tests.helpers import E2E, e2e_corpus, e2e_heldin
 pytestmark = pytest.mark.gpu
 
 
-def test_gpu_hogwild_end_to_end_metrics_within_one_percent_of_sequential(tmp_path):
-    with open(os.path.join(GOLDEN, "e2e_parity.json")) as f:
-        ref = json.load(f)
+def _train_e2e(tmp_path, sample, grid=None):
+    """the reference's 10-iteration flow on the GPU, every seed of the golden
+    run; returns per-seed metrics and the grids (set_vocab's, last call's)"""
     tok, counts, index2word, lines, perms, wseeds = e2e_corpus()
-    assert zlib.crc32(tok.tobytes()) == ref["corpus_crc32"]
     n = len(tok) // 2
-    D, K, sample = E2E["D"], E2E["K"], E2E["sample"]
+    D, K = E2E["D"], E2E["K"]
     V = len(counts)
     syn0 = E.seeded_vectors(wseeds, D)
     js = E.plan_jobs(n_sent=n, sent_len=2)
     al = E.job_alphas(js, n)
-    got = {"loss": [], "heldin": [], "target_ratio": []}
+    got = {"loss": [], "heldin": [], "target_ratio": [], "grid": [], "call_grid": []}
     for seed in E2E["seeds"]:
         eng = E.SGNSEngine(V, D, K)
+        if grid:
+            eng.set_option(N.OPT_GRID, grid)
         eng.set_vocab(counts, sample)
         eng.set_weights(syn0, np.zeros_like(syn0))
         rs = np.random.RandomState(seed)
@@ -57,7 +58,9 @@ def test_gpu_hogwild_end_to_end_metrics_within_one_percent_of_sequential(tmp_pat
                 eng.reset_loss()
             eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD, compute_loss=last)
         eng.sync()
-        loss = eng.read_stats()["training_loss"]
+        st = eng.read_stats()
+        got["grid"].append(int(eng.get_option(N.OPT_GRID)))
+        got["call_grid"].append(int(st["sgns_grid"]))
         s0, s1 = eng.get_weights()
         eng.close()
         kv = KeyedVectors(D)
@@ -67,11 +70,48 @@ def test_gpu_hogwild_end_to_end_metrics_within_one_percent_of_sequential(tmp_pat
         w2v = str(tmp_path / f"seed{seed}_w2v.txt")
         kv.save_word2vec_format(w2v)
         t = EV.target_function(w2v, pathways=lines, strict=False, verbose=False)
-        got["loss"].append(float(loss))
+        got["loss"].append(float(st["training_loss"]))
         got["heldin"].append(e2e_heldin(s0, s1, tok, counts, K))
         got["target_ratio"].append(float(t["ratio"]))
-    gaps = {k: (np.mean(v) - ref[k + "_mean"]) / ref[k + "_mean"] for k, v in got.items()}
+    return got
+
+
+def _gaps(got, ref):
+    return {k: (np.mean(got[k]) - ref[k + "_mean"]) / ref[k + "_mean"]
+            for k in ("loss", "heldin", "target_ratio")}
+
+
+def _golden():
+    with open(os.path.join(GOLDEN, "e2e_parity.json")) as f:
+        ref = json.load(f)
+    tok = e2e_corpus()[0]
+    assert zlib.crc32(tok.tobytes()) == ref["corpus_crc32"]
+    return ref
+
+
+def test_gpu_hogwild_end_to_end_metrics_within_one_percent_of_sequential(tmp_path):
+    ref = _golden()
+    got = _train_e2e(tmp_path, E2E["sample"])
+    gaps = _gaps(got, ref)
     print("gpu", got, "gaps vs sequential oracle", gaps)
     assert abs(gaps["loss"]) < 0.01, gaps
     assert abs(gaps["heldin"]) < 0.005, gaps
     assert abs(gaps["target_ratio"]) < 0.01, gaps
+
+
+def test_gpu_hogwild_sample0_stays_stable(tmp_path):
+    """sample = 0 keeps the hottest genes' syn0 rows busy: past a staleness
+    that grows with the vectors' norms a hot syn0 row overshoots at a
+    sawtooth restart and freezes (|f| >= 6 skips every later update; DESIGN.md
+    5c).  g2v_train caps each call's grid for it (stability_grid): the
+    objective and the final loss track the sequential oracle's, and the cap
+    has engaged by the last call.  The target function is reported, not
+    gated: at sample 0 the Hogwild staleness moves it a few percent on
+    structured corpora."""
+    ref = _golden()["sample0"]
+    got = _train_e2e(tmp_path, 0.0)
+    gaps = _gaps(got, ref)
+    print("gpu sample 0", got, "gaps vs sequential oracle", gaps)
+    assert all(c < g for c, g in zip(got["call_grid"], got["grid"])), got
+    assert abs(gaps["heldin"]) < 0.005, gaps
+    assert abs(gaps["loss"]) < 0.01, gaps
