@@ -1231,8 +1231,8 @@ static int stability_grid(g2v_ctx* c, const float* job_alpha, int64_t n_jobs) {
   const double per_wave = c->p_tok_max * (c->K + 1) * amax * k1;
   if (per_wave <= 0.0) return G2V_OK;
   const double waves = kSyn0Budget / per_wave;
-  const int cap = (int)std::max(1.0, std::floor(waves / c->active_waves));
-  if (cap < c->sgns_grid) c->call_grid = cap;
+  if (waves >= (double)c->sgns_grid * c->active_waves) return G2V_OK;  // the default is within it
+  c->call_grid = (int)std::max(1.0, std::floor(waves / c->active_waves));
   return G2V_OK;
 }
 
