@@ -240,6 +240,11 @@ def main(argv=None):
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
                              "collective (gloo) = auto; torch = torch-owned tables merged by "
                              "torch.distributed")
+    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=10_000_000,
+                        help="under torchrun, shard the pairs only when every rank gets at least "
+                             "this many; a smaller corpus trains whole on every rank (no merges, "
+                             "rank 0 writes): merged replicas of small shards learn far less "
+                             "than one model (DESIGN.md 7b)")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "
@@ -305,6 +310,13 @@ def main(argv=None):
         shuffle_mode = "python"
         if corpus is not None:
             pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
+    # data parallelism only for corpora big enough that merged replicas match
+    # one model; below, every rank trains the whole corpus
+    shard = world > 1 and n_pairs >= world * args.dp_min_pairs_per_rank
+    if world > 1 and not shard:
+        print(f"{n_pairs} pairs < {world} ranks x {args.dp_min_pairs_per_rank}: every rank "
+              "trains the whole corpus (no sharding, no merges); rank 0 writes the outputs")
+    drank, dworld = (rank, world) if shard else (0, 1)
     dorder = None
     perm_seed = None
     print(datetime.datetime.now())
@@ -336,7 +348,7 @@ def main(argv=None):
         outputs = []
         kw = dict(size=dimension, window=args.window, min_count=1, workers=args.workers, iter=1,
                   sg=1, negative=args.negative, sample=args.sample, hashfxn=hashfxn,
-                  device=args.device, mode=args.mode, data_parallel=world > 1)
+                  device=args.device, mode=args.mode, data_parallel=shard)
         import gene2vec_amd.word2vec as W
         W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
         W.DP_MERGE_TRANSPORT = args.merge_transport
@@ -364,7 +376,7 @@ def main(argv=None):
                     with ph("train"):
                         if shuffle_mode == "device":
                             dorder = _DeviceOrder(tok, _vocab_ids(model, corpus), args.device,
-                                                  rank, world)
+                                                  drank, dworld)
                             model.train_ids(None, None, 2, total_examples=model.corpus_count,
                                             epochs=model.iter,
                                             device_tokens=dorder.shard(perm_seed))
@@ -400,7 +412,7 @@ def main(argv=None):
                     # its RCCL communicator and the merge snapshot carry over.
                     if args.reload_checkpoints or model is None:
                         model = Word2Vec.load(prev, device=args.device)
-                        model.data_parallel = world > 1
+                        model.data_parallel = shard
                 if corpus is None:
                     with ph("train"):
                         model.train(gene_pairs, total_examples=model.corpus_count,
@@ -416,7 +428,7 @@ def main(argv=None):
                             # another vocabulary numbering: the resident order is
                             # re-uploaded (the model keeps its vocabulary, so never
                             # in the reference's loop)
-                            dorder = _DeviceOrder(tok, ids, args.device, rank, world)
+                            dorder = _DeviceOrder(tok, ids, args.device, drank, dworld)
                     with ph("train"):
                         if dorder is not None:
                             model.train_ids(None, None, 2, total_examples=model.corpus_count,

@@ -216,6 +216,9 @@ def main():
     ap.add_argument("--single-seeds", default="1",
                     help="model.random seeds of the one-model runs (several: the one model's "
                          "own run-to-run spread, the yardstick for the replica gaps)")
+    ap.add_argument("--oracle", action="store_true",
+                    help="also train the sequential C oracle (gensim workers=1 order) on the same "
+                         "permutations and job seeds as the first one-model run")
     ap.add_argument("--out", default="gpurun_out/replica_quality")
     a = ap.parse_args()
     import torch
@@ -306,6 +309,24 @@ def main():
         finish("single" if si == 0 else f"single_seed{sseed}", s0, s1,
                {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
 
+    # ---- the sequential oracle (gensim's workers=1 order) -----------------------------
+    if a.oracle:
+        from oracle import c_oracle as CO
+        a0, a1 = syn0.copy(), np.zeros_like(syn0)
+        rs = np.random.RandomState(int(a.single_seeds.split(",")[0]))
+        js = E.plan_jobs(n_sent=n, sent_len=2)
+        al = E.job_alphas(js, n).astype(np.float32)
+        off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
+        si, cum = CO.sample_int(vc, a.sample), CO.make_cum_table(vc)
+        t = time.time()
+        for it in range(a.iters):
+            permute(it)
+            tk = perm.cpu().numpy().view(np.int32)
+            CO.train(tk, off, js, al, E.job_seeds(rs, len(js) - 1), si, a.sample != 0, cum, a0,
+                     a1, np.ones(V, np.float32), K)
+            print("oracle iter", it, round(heldin(a0, a1, tok, vc, K, n=20000), 5), flush=True)
+        finish("oracle", a0, a1, {"train_s": round(time.time() - t, 1)})
+
     # ---- R replicas, libg2v merge every c jobs ---------------------------------------
     def parse_rule(r):
         """'mean', 'touch:B:G', 'align:B:G' (B, G = beta, gamma x 1000) or 'B:G' (touch)"""
@@ -369,21 +390,27 @@ def main():
                + (f"_gamma{gamma}" if gamma != 1000 else ""), s0, s1,
                {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it,
                 "merges_total": merges, "replicas_identical": same})
-    if "single" in log["runs"]:
-        ref = log["runs"]["single"]
+    for ref_tag in ("single", "oracle"):
+        if ref_tag not in log["runs"]:
+            continue
+        ref = log["runs"][ref_tag]
+        sfx = "" if ref_tag == "single" else "_vs_oracle"
         for tag, r in log["runs"].items():
-            if tag != "single":  # gaps to the first one-model run
-                r["heldin_gap"] = round((r["heldin"] - ref["heldin"]) / ref["heldin"], 5)
-                r["heldout_gap"] = round((r["heldout"] - ref["heldout"]) / ref["heldout"], 5)
+            if tag != ref_tag:  # gaps to the reference run
+                r["heldin_gap" + sfx] = round((r["heldin"] - ref["heldin"]) / ref["heldin"], 5)
+                r["heldout_gap" + sfx] = round((r["heldout"] - ref["heldout"]) / ref["heldout"],
+                                               5)
                 if "auc_mean" in r and "auc_mean" in ref:
-                    r["auc_gap"] = round((r["auc_mean"] - ref["auc_mean"]) / ref["auc_mean"], 5)
-                    r["target_gap"] = round((r["target_ratio"] - ref["target_ratio"])
-                                            / ref["target_ratio"], 5)
+                    r["auc_gap" + sfx] = round((r["auc_mean"] - ref["auc_mean"])
+                                               / ref["auc_mean"], 5)
+                    r["target_gap" + sfx] = round((r["target_ratio"] - ref["target_ratio"])
+                                                  / ref["target_ratio"], 5)
         json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
     for tag, r in log["runs"].items():
-        print(tag, {k: r[k] for k in ("heldin", "heldin_gap", "heldout", "heldout_gap",
-                                      "auc_mean", "auc_gap",
-                                      "target_ratio", "target_gap") if k in r})
+        print(tag, {k: r[k] for k in ("heldin", "heldin_gap", "heldin_gap_vs_oracle", "heldout",
+                                      "heldout_gap", "heldout_gap_vs_oracle", "auc_mean",
+                                      "auc_gap", "auc_gap_vs_oracle", "target_ratio",
+                                      "target_gap", "target_gap_vs_oracle") if k in r})
     print(json.dumps(log))
 
 

@@ -66,7 +66,7 @@ def test_cli_data_parallel_two_ranks(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
-           "--backend", "gloo", "--merge-transport", "host"] + opts
+           "--backend", "gloo", "--merge-transport", "host", "--dp-min-pairs-per-rank", "0"] + opts
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
 
@@ -106,7 +106,8 @@ def test_cli_data_parallel_replicas_identical(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
-           "--backend", "gloo", "--iters", "3", "--dim", "32", "--hash", "crc32",
+           "--backend", "gloo", "--dp-min-pairs-per-rank", "0", "--iters", "3", "--dim", "32",
+           "--hash", "crc32",
            "--shuffle-seed", "3", "--native-ingest", "--no-txt", "--no-w2v",
            "--merge-every-jobs", "4"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
@@ -137,7 +138,8 @@ def test_cli_data_parallel_ragged_corpus_falls_back(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
-           "--backend", "gloo", "--iters", "2", "--dim", "16", "--hash", "crc32",
+           "--backend", "gloo", "--dp-min-pairs-per-rank", "0", "--iters", "2", "--dim", "16",
+           "--hash", "crc32",
            "--shuffle-seed", "2", "--native-ingest", "--no-txt", "--no-w2v",
            "--merge-transport", "torch"]
     r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
@@ -145,3 +147,36 @@ def test_cli_data_parallel_ragged_corpus_falls_back(tmp_path):
     assert "using Python's shuffle" in r.stdout
     m = Word2Vec.load(str(tmp_path / "dp" / "gene2vec_dim_16_iter_2"))
     assert m.corpus_count == 40_000 and np.isfinite(m.wv.vectors).all()
+
+
+def test_cli_small_corpus_trains_whole_on_every_rank(tmp_path):
+    """below --dp-min-pairs-per-rank (default 10 M) the CLI does not shard:
+    merged replicas of small shards learn far less than one model (DESIGN.md
+    7b: 8 x 1.25 M pairs, 10 iterations, held-in objective +36 %), so every
+    rank trains the whole corpus and rank 0's outputs match a single-process
+    run (same shuffles, Hogwild noise only)"""
+    V, n_pairs = 1000, 200_000
+    names = S.gene_names(V)
+    pairs = S.zipf_gene_pairs(n_pairs, V, 1.0, seed=13)
+    data = tmp_path / "data"
+    data.mkdir()
+    (data / "pairs.txt").write_text(
+        "\n".join(f"{names[a]} {names[b]}" for a, b in pairs) + "\n", encoding="windows-1252")
+    opts = ["--iters", "3", "--dim", "32", "--hash", "crc32", "--shuffle-seed", "7",
+            "--native-ingest", "--no-txt"]
+    cli_main([str(data), str(tmp_path / "single"), "txt", "--shuffle", "device"] + opts)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
+               PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "gene2vec_amd.gene2vec", str(data), str(tmp_path / "dp"), "txt",
+           "--backend", "gloo"] + opts
+    r = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "every rank trains the whole corpus" in r.stdout
+    single = Word2Vec.load(str(tmp_path / "single" / "gene2vec_dim_32_iter_3"))
+    dp = Word2Vec.load(str(tmp_path / "dp" / "gene2vec_dim_32_iter_3"))
+    assert dp.wv.index2word == single.wv.index2word
+    l1, l2 = _heldin_loss(single, pairs, names), _heldin_loss(dp, pairs, names)
+    print("held-in SGNS objective: single %.4f data-parallel CLI, unsharded %.4f" % (l1, l2))
+    assert abs(l2 - l1) / l1 < 0.005, (l1, l2)
