@@ -240,7 +240,7 @@ def main(argv=None):
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
                              "collective (gloo) = auto; torch = torch-owned tables merged by "
                              "torch.distributed")
-    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=10_000_000,
+    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=125_000_000,
                         help="under torchrun, shard the pairs only when every rank gets at least "
                              "this many; a smaller corpus trains whole on every rank (no merges, "
                              "rank 0 writes): merged replicas of small shards learn far less "
