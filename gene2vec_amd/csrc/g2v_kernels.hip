@@ -348,24 +348,35 @@ __global__ void k_fold_stripes(float* syn0, float* syn1, float* stripe, int rows
 }
 
 // largest squared row norm of a [V][ld] table (the Hogwild stability cap of
-// g2v_train): one wave per row, the float bits of a non-negative sum ordered
-// like unsigned integers, so one atomicMax keeps the maximum
+// g2v_train): waves stride over the rows keeping a running maximum, the
+// workgroup's maximum goes out as one atomicMax on the float bits (a
+// non-negative float orders like its unsigned bits) -- 256 atomics on one word,
+// not one per row
+constexpr int kNormBlocks = 256;
 __global__ void k_row_norm2_max(const float* t, int V, int64_t ld, int D, unsigned int* out) {
+  __shared__ float s_max[4];
   const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (r >= V) return;
-  const float* row = t + r * ld;
-  float s = 0.f;
-  for (int i = lane; i < D; i += 64) s = fmaf(row[i], row[i], s);
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  if (lane == 0) atomicMax(out, __float_as_uint(s));
+  const int w = threadIdx.x >> 6;
+  const int64_t waves = (int64_t)gridDim.x * 4;
+  float m = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * 4 + w; r < V; r += waves) {
+    const float* row = t + r * ld;
+    float s = 0.f;
+    for (int i = lane; i < D; i += 64) s = fmaf(row[i], row[i], s);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    m = fmaxf(m, s);
+  }
+  if (lane == 0) s_max[w] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(out, __float_as_uint(fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]))));
 }
 
 hipError_t launch_row_norm2_max(const float* t, int V, int64_t ld, int D, unsigned int* out,
                                 hipStream_t st) {
   if (V <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_row_norm2_max, dim3((unsigned)((V + 3) / 4)), dim3(256), 0, st, t, V, ld, D,
-                     out);
+  const int blocks = (int)std::min<int64_t>(kNormBlocks, ((int64_t)V + 3) / 4);
+  hipLaunchKernelGGL(k_row_norm2_max, dim3((unsigned)blocks), dim3(256), 0, st, t, V, ld, D, out);
   return hipGetLastError();
 }
 
