@@ -121,11 +121,15 @@ E2E = {"V0": 3000, "modules": 100, "p_in": 0.5, "pairs": 2_000_000, "iters": 10,
        "K": 5, "sample": 1e-3, "seeds": (1, 2, 3)}
 
 
-def e2e_corpus():
+# the same flow at the C2 bench vocabulary (tests/golden/e2e_parity_c2.json)
+E2E_C2 = dict(E2E, V0=24447, modules=1000, pairs=10_000_000, seeds=(1, 2))
+
+
+def e2e_corpus(c=None):
     """(tok int32[2n] in vocab index order, vocab counts, index2word, pathway
     lines (gmt text, newline kept as the reference reads them), per-iteration
-    permutations, seeded syn0)"""
-    c = E2E
+    permutations, seeded syn0 hashes)"""
+    c = c or E2E
     V0, M = c["V0"], c["modules"]
     pairs = zipf_pairs(c["pairs"], V0, 1.0, seed=20250114)
     mod = np.empty(V0, np.int64)

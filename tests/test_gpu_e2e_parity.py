@@ -27,31 +27,31 @@ from gene2vec_amd import engine as E
 from gene2vec_amd import evaluate as EV
 from gene2vec_amd.word2vec import KeyedVectors, Vocab
 from tests.conftest import GOLDEN
-from tests.helpers import E2E, e2e_corpus, e2e_heldin
+from tests.helpers import E2E, E2E_C2, e2e_corpus, e2e_heldin
 
 pytestmark = pytest.mark.gpu
 
 
-def _train_e2e(tmp_path, sample, grid=None):
+def _train_e2e(tmp_path, sample, grid=None, cfg=E2E):
     """the reference's 10-iteration flow on the GPU, every seed of the golden
     run; returns per-seed metrics and the grids (set_vocab's, last call's)"""
-    tok, counts, index2word, lines, perms, wseeds = e2e_corpus()
+    tok, counts, index2word, lines, perms, wseeds = e2e_corpus(cfg)
     n = len(tok) // 2
-    D, K = E2E["D"], E2E["K"]
+    D, K = cfg["D"], cfg["K"]
     V = len(counts)
     syn0 = E.seeded_vectors(wseeds, D)
     js = E.plan_jobs(n_sent=n, sent_len=2)
     al = E.job_alphas(js, n)
     got = {"loss": [], "heldin": [], "target_ratio": [], "grid": [], "call_grid": []}
-    for seed in E2E["seeds"]:
+    for seed in cfg["seeds"]:
         eng = E.SGNSEngine(V, D, K)
         if grid:
             eng.set_option(N.OPT_GRID, grid)
         eng.set_vocab(counts, sample)
         eng.set_weights(syn0, np.zeros_like(syn0))
         rs = np.random.RandomState(seed)
-        for it in range(E2E["iters"]):
-            last = it == E2E["iters"] - 1
+        for it in range(cfg["iters"]):
+            last = it == cfg["iters"] - 1
             eng.set_corpus(np.ascontiguousarray(tok.reshape(n, 2)[perms[it]].reshape(-1)),
                            sent_len=2)
             if last:
@@ -81,10 +81,10 @@ def _gaps(got, ref):
             for k in ("loss", "heldin", "target_ratio")}
 
 
-def _golden():
-    with open(os.path.join(GOLDEN, "e2e_parity.json")) as f:
+def _golden(name="e2e_parity.json", cfg=E2E):
+    with open(os.path.join(GOLDEN, name)) as f:
         ref = json.load(f)
-    tok = e2e_corpus()[0]
+    tok = e2e_corpus(cfg)[0]
     assert zlib.crc32(tok.tobytes()) == ref["corpus_crc32"]
     return ref
 
@@ -115,3 +115,18 @@ def test_gpu_hogwild_sample0_stays_stable(tmp_path):
     assert all(c < g for c, g in zip(got["call_grid"], got["grid"])), got
     assert abs(gaps["heldin"]) < 0.005, gaps
     assert abs(gaps["loss"]) < 0.01, gaps
+
+
+def test_gpu_end_to_end_at_the_c2_vocabulary(tmp_path):
+    """the same gate at the bench's vocabulary (24,447 Zipf genes, 1,000
+    planted modules, 10 M pairs, sample 1e-3), the production defaults (one
+    workgroup per CU); golden from the sequential oracle, two seeds
+    (tests/golden/make_e2e_golden.py --c2).  Measured: loss +0.07 %,
+    objective -0.01 %, target function -0.10 %."""
+    ref = _golden("e2e_parity_c2.json", E2E_C2)
+    got = _train_e2e(tmp_path, E2E_C2["sample"], cfg=E2E_C2)
+    gaps = _gaps(got, ref)
+    print("gpu C2 vocabulary", got, "gaps vs sequential oracle", gaps)
+    assert abs(gaps["loss"]) < 0.01, gaps
+    assert abs(gaps["heldin"]) < 0.005, gaps
+    assert abs(gaps["target_ratio"]) < 0.01, gaps
