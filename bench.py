@@ -17,8 +17,9 @@ RCCL unique id).  N = 1 runs no merge at all.
 
 Prints ONE JSON line on rank 0 (see the contract in the task description):
 value = pairs/s over all ranks, plus `roofline` (dominant kernel =
-k_sgns_atomic, algorithmic bytes 2*(K+2)*D*4 per directed example / its
-average launch time, HIP events on the launch stream) and `cpu_baseline`
+k_sgns_atomic, bound = memory-side float atomics: algorithmic atomic bytes
+(K+2)*D*4 per directed example / its average launch time, HIP events on the
+launch stream; the HBM view, 2*(K+2)*D*4 bytes, beside it) and `cpu_baseline`
 (the C oracle, Hogwild OpenMP, on a bounded sample of the same corpus).
 """
 from __future__ import annotations
@@ -40,6 +41,7 @@ import numpy as np  # noqa: E402
 METRIC = "gene pairs/sec (SGNS dim200 neg5) at 1/2/4/8 MI355X + achieved GB/s"
 # BASELINE.json configs[3] (C4): python bench.py --vocab 60000 --dim 512 --negative 15
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+ATOMIC_PEAK_GBPS = 1300.0  # MI355X_MICROARCH.md "Global float atomics": chip-wide added bytes
 
 
 def usable_cpus():
@@ -101,9 +103,12 @@ def parse():
     p.add_argument("--backend", choices=("nccl", "gloo"), default="nccl",
                    help="process-group backend (nccl = RCCL over xGMI; gloo only to rehearse "
                         "the N>1 path with several ranks sharing one GPU)")
-    p.add_argument("--merge-transport", choices=("auto", "torch"), default="auto",
+    p.add_argument("--merge-transport", choices=("auto", "rccl", "torch"), default="auto",
                    help="N>1: auto = libg2v's merge over RCCL (nccl) or over the host "
-                        "collective (gloo); torch = torch.distributed merges the bound tables")
+                        "collective (gloo); rccl = libg2v's RCCL communicator whatever the "
+                        "process group (with gloo: the test suite's two-ranks-one-GPU "
+                        "stand-in, G2V_RCCL_LIB); torch = torch.distributed merges the bound "
+                        "tables")
     p.add_argument("--traffic-json", default=None,
                    help="PMC bytes per example for roofline.traffic (default: the newest "
                         "profiles/**/traffic_r*.json of this workload measured on this kernel build)")
@@ -202,7 +207,8 @@ def main():
     avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
     merge_backend = "torch"
     merge_note = None
-    if use_dist and a.backend == "nccl" and a.merge_transport == "auto":
+    if use_dist and ((a.backend == "nccl" and a.merge_transport == "auto")
+                     or a.merge_transport == "rccl"):
         # libg2v's own RCCL communicator: rank 0's unique id over the process group
         box = [eng.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(box, src=0)
@@ -211,7 +217,8 @@ def main():
             merge_backend = "rccl"
         except N.G2VError as e:  # keep the run measurable: torch merges the bound tables
             merge_note = f"g2v_comm_init failed ({e}); torch.distributed merge used"
-        ok = torch.tensor([1 if merge_backend == "rccl" else 0], device=dev)
+        ok = torch.tensor([1 if merge_backend == "rccl" else 0],
+                          device=dev if a.backend == "nccl" else "cpu")
         dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if ok.item() == 0:  # every rank must merge the same way
             merge_backend = "torch"
@@ -280,10 +287,13 @@ def main():
     # examples per launch; a profile of another build is refused (traffic null)
     from gene2vec_amd.build import kernel_source_hash
     ksha = kernel_source_hash()
-    launch = {"grid_workgroups": eng.get_option(N.OPT_GRID),
-              "stripes": f"{eng.get_option(N.OPT_STRIPE_ROWS)}x{eng.get_option(N.OPT_STRIPE_COPIES)}",
-              "stripes_tier2": f"rows < {eng.get_option(N.OPT_STRIPE2_ROWS)} "
-                               f"x{eng.get_option(N.OPT_STRIPE2_COPIES)}"}
+    # the layout the timed launches actually used (g2v_stats: the per-call
+    # stability cap may lower the grid below set_vocab's, which also changes
+    # the default stripe tiers), not the options' nominal values
+    launch = {"grid_workgroups": st["sgns_grid"],
+              "stripes": f"{st['stripe_rows']}x{st['stripe_copies']}",
+              "stripes_tier2": (f"rows < {st['stripe2_rows']} x{st['stripe2_copies']}"
+                                if st["stripe2_copies"] > 1 else "off")}
     cands = [a.traffic_json] if a.traffic_json else sorted(
         glob.glob(os.path.join(ROOT, "profiles", "**", "traffic_r*.json"), recursive=True),
         reverse=True)
@@ -315,15 +325,25 @@ def main():
     atomic_bytes = (K + 2) * D * 4  # every SGNS update is a memory-side f32 atomic delta
     atomic_gbps = atomic_bytes * st["examples"] / (st["sgns_kernel_ms"] / 1e3) / 1e9 \
         if st["sgns_kernel_ms"] > 0 else 0.0
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic,
+    # bound = the resource that binds k_sgns_atomic: every table update is a
+    # memory-side f32 atomic (MI355X_MICROARCH.md "Global float atomics": ~1.3
+    # TB/s of added bytes chip-wide, whatever the placement); achieved = the
+    # algorithmic atomic bytes (K+2)*D*4 per directed example / launch time.
+    # The HBM view of the same launches (2*(K+2)*D*4 bytes per example: every
+    # updated row read and written) stays beside it as hbm_*.
+    roofline = {"bound": "atomics", "achieved": round(atomic_gbps, 1), "peak": ATOMIC_PEAK_GBPS,
+                "unit": "GB/s", "frac": round(atomic_gbps / ATOMIC_PEAK_GBPS, 4),
+                "traffic": traffic,
                 "kernel": "k_sgns_atomic", "avg_launch_ms": round(avg_launch_ms, 4),
+                "atomic_bytes_per_example": atomic_bytes,
                 "algorithmic_bytes_per_launch": int(alg_bytes_launch),
                 "bytes_per_example": bytes_per_example,
                 "binding_resource": "memory-side float atomics (MI355X_MICROARCH.md: ~1300 GB/s "
                                     "of added bytes chip-wide)",
-                "atomic_achieved_GBps": round(atomic_gbps, 1), "atomic_peak_GBps": 1300.0,
-                "atomic_frac": round(atomic_gbps / 1300.0, 4), "traffic_source": traffic_src,
+                "hbm_achieved_GBps": round(achieved, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
+                "hbm_frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                "traffic_source": traffic_src,
                 "kernel_src_sha16": ksha,
                 **launch}
 
@@ -422,7 +442,9 @@ def main():
                             (f"C3: synthetic Zipf gene pairs, V={V0}, {n_pairs} pairs per GPU x "
                              f"{world}, dim {D}, neg {K}, replica merge ({a.merge}) every "
                              f"{avg_every} jobs: "
-                             + ("libg2v g2v_average (RCCL over xGMI)" if merge_backend == "rccl"
+                             + (("libg2v g2v_average (RCCL over xGMI)" if a.backend == "nccl"
+                                 else "libg2v RCCL merge path through G2V_RCCL_LIB (rehearsal, "
+                                      "ranks sharing a GPU)") if merge_backend == "rccl"
                                 else "libg2v merge over gloo (host collective) rehearsal, ranks "
                                      "sharing a GPU" if merge_backend == "libg2v-host"
                                 else "torch.distributed gloo rehearsal, ranks sharing a GPU"

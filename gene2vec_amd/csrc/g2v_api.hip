@@ -150,6 +150,7 @@ struct g2v_ctx {
   int atomic_overlap = 1;
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
+  int64_t debug_fail_merge = 0;  // G2V_OPT_DEBUG_FAIL_MERGE: fault injection
   int merge_rule = 0;
   float merge_beta = 1.0f;   // G2V_OPT_MERGE_BETA_MILLI / 1000
   float merge_gamma = 1.0f;  // G2V_OPT_MERGE_GAMMA_MILLI / 1000
@@ -333,6 +334,7 @@ struct Rccl {
   decltype(&ncclGroupEnd) group_end = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   std::string load_error;
+  std::string library;  // what was dlopen()ed
 };
 
 const Rccl& rccl() {
@@ -340,11 +342,24 @@ const Rccl& rccl() {
   static std::once_flag once;
   std::call_once(once, [] {
     void* h = nullptr;
-    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
-      if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+    // G2V_RCCL_LIB names another library with RCCL's entry points and nothing
+    // else is tried (the test suite's stand-in, tests/rccl_standin/: two
+    // ranks on ONE GPU, which real RCCL refuses as "Duplicate GPU")
+    const char* over = getenv("G2V_RCCL_LIB");
+    if (over && *over) {
+      h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
+      r.library = over;
+    } else {
+      for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+        if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) {
+          r.library = name;
+          break;
+        }
+    }
     if (!h) {
       const char* e = dlerror();
-      r.load_error = std::string("dlopen(librccl.so.1) failed: ") + (e ? e : "?");
+      r.load_error = std::string("dlopen(") + (over && *over ? over : "librccl.so.1") +
+                     ") failed: " + (e ? e : "?");
       return;
     }
     bool ok = true;
@@ -362,7 +377,7 @@ const Rccl& rccl() {
     sym(r.error_string, "ncclGetErrorString");
     if (!ok) {
       r.get_unique_id = nullptr;
-      r.load_error = "librccl.so.1 lacks an nccl* entry point";
+      r.load_error = r.library + " lacks an nccl* entry point";
     }
     r.comm_abort = reinterpret_cast<decltype(&ncclCommAbort)>(dlsym(h, "ncclCommAbort"));
   });
@@ -667,6 +682,10 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
               "merge gamma (x1000) out of [1000, 16000]");
       c->merge_gamma = (float)value / 1000.0f;
       return G2V_OK;
+    case G2V_OPT_DEBUG_FAIL_MERGE:
+      REQUIRE(value >= 0, G2V_EINVAL, "debug fail merge < 0");
+      c->debug_fail_merge = value;
+      return G2V_OK;
     case G2V_OPT_ACTIVE_WAVES:
       REQUIRE(value >= 1 && value <= kSgnsThreads / 64, G2V_EINVAL, "active waves out of [1, %d]",
               kSgnsThreads / 64);
@@ -696,6 +715,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_ACTIVE_WAVES: *out = c->active_waves; return G2V_OK;
     case G2V_OPT_MERGE_BETA_MILLI: *out = (int64_t)lrintf(c->merge_beta * 1000.0f); return G2V_OK;
     case G2V_OPT_MERGE_GAMMA_MILLI: *out = (int64_t)lrintf(c->merge_gamma * 1000.0f); return G2V_OK;
+    case G2V_OPT_DEBUG_FAIL_MERGE: *out = c->debug_fail_merge; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -1281,12 +1301,19 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
     }
   }
   const int64_t n_seg = (int64_t)segs.size();
+  int64_t merges = 0;
+  auto merge = [&]() -> int {
+    if (++merges == c->debug_fail_merge)
+      return fail(G2V_ECOMM, "injected failure before in-call merge %lld (G2V_OPT_DEBUG_FAIL_MERGE)",
+                  (long long)merges);
+    return merge_now(c, c->merge_rule);
+  };
   if (!c->sample_overlap || n_seg == 1) {
     for (const Seg& g : segs) {
       if ((rc = sample_segment(c, g.j0, g.nj, timing))) return rc;
       if ((rc = run_sgns(c, c->d_job_exoff + g.nj, mode, timing, closs, c->syn0, c->syn1)))
         return rc;
-      if (g.merge && (rc = merge_now(c, c->merge_rule))) return rc;
+      if (g.merge && (rc = merge())) return rc;
     }
     c->jobs += n_jobs;
     return G2V_OK;
@@ -1319,7 +1346,7 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
                        c->syn0, c->syn1, b ? c->d_rec2 : c->d_rec)))
       return rc;
     HIPCHK(hipEventRecord(c->ev_sgns[b], c->stream));
-    if (g.merge && (rc = merge_now(c, c->merge_rule))) return rc;
+    if (g.merge && (rc = merge())) return rc;
   }
   c->jobs += n_jobs;
   return G2V_OK;
@@ -1635,15 +1662,27 @@ int g2v_comm_init_local(g2v_ctx* c, g2v_local_group* g, int rank) {
       g->cv.notify_all();
       return fail(G2V_EINVAL, "rank %d: device / V / ld differ from the group's", rank);
     }
-    REQUIRE(!g->joined[(size_t)rank], G2V_EINVAL, "rank %d joined twice", rank);
+    // every failure from here on aborts the group (under its lock), so the
+    // ranks already waiting in local_broadcast's barrier fail at once
+    auto abort_locked = [&](int code) {
+      g->aborted = true;
+      g->why = g_err;
+      g->cv.notify_all();
+      return code;
+    };
+    if (g->joined[(size_t)rank])
+      return abort_locked(fail(G2V_EINVAL, "rank %d joined twice", rank));
     g->joined[(size_t)rank] = 1;
-    if (!g->ev[(size_t)rank])
-      HIPCHK(hipEventCreateWithFlags(&g->ev[(size_t)rank], hipEventDisableTiming));
+    hipError_t he = hipSuccess;
+    if (!g->ev[(size_t)rank] &&
+        (he = hipEventCreateWithFlags(&g->ev[(size_t)rank], hipEventDisableTiming)) != hipSuccess)
+      return abort_locked(fail(G2V_EHIP, "hipEventCreate failed: %s", hipGetErrorString(he)));
     if (rank == 0) {
-      HIPCHK(hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming));
+      if ((he = hipEventCreateWithFlags(&g->ev_done, hipEventDisableTiming)) != hipSuccess)
+        return abort_locked(fail(G2V_EHIP, "hipEventCreate failed: %s", hipGetErrorString(he)));
       // both tables and both touched-count vectors of one merge
       const size_t need = 2 * (size_t)c->V * (size_t)c->ld + 4 * (size_t)c->V;
-      if ((rc = dev_alloc(&g->scratch, need))) return rc;
+      if ((rc = dev_alloc(&g->scratch, need))) return abort_locked(rc);
       g->scratch_cap = need;
     }
   }

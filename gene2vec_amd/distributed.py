@@ -123,31 +123,77 @@ def touch_merge_(tensors, olds, beta=1.0, group=None, align=False, gamma=1.0):
         t.copy_(old)
 
 
-def host_collective(group=None):
+class PeerFailed(RuntimeError):
+    """a peer joined a host collective with its ok flag cleared"""
+
+
+class HostCollective:
     """The collective of g2v_comm_init_host over torch.distributed (gloo):
     op(COLL_SUM) gathers every rank's buffer and adds them in rank order from
     zero -- the order of the in-process group's device sum and of
     g2v_average_local, so the merged bits do not depend on gloo's reduction
-    schedule; op(COLL_BCAST0) takes rank 0's buffer."""
-    import torch
-    import torch.distributed as dist
+    schedule; op(COLL_BCAST0) takes rank 0's buffer.
 
-    from . import _native as N
+    Every SUM carries one more float, the rank's ok flag.  A host collective
+    blocks the caller inside g2v_train (unlike RCCL's, which are only
+    enqueued), so a rank whose training call fails between two in-call
+    merges leaves its peers waiting in the next one; it must join that
+    collective (``fail_pending``) with the flag cleared, and the peers then
+    fail it (PeerFailed -> G2V_ECOMM) instead of running a mismatched gloo
+    collective against the failing rank's later agreement."""
 
-    def run(op, buf):
-        t = torch.from_numpy(buf)  # shares the pinned staging buffer
+    def __init__(self, group=None):
+        self.group = group
+        self.sums = 0  # SUM collectives completed on this rank
+
+    def _sum(self, buf, ok):
+        import torch
+        import torch.distributed as dist
+        n = buf.size
+        ext = torch.empty(n + 1, dtype=torch.float32)
+        ext[:n] = torch.from_numpy(buf)
+        ext[n] = 1.0 if ok else 0.0
+        parts = [torch.empty_like(ext) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(parts, ext, group=self.group)
+        bad = [r for r, p in enumerate(parts) if float(p[n]) != 1.0]
+        if bad:
+            raise PeerFailed(f"rank(s) {bad} failed before this replica merge")
+        s = torch.zeros(n, dtype=torch.float32)
+        for p in parts:
+            s += p[:n]
+        torch.from_numpy(buf).copy_(s)
+        self.sums += 1
+
+    def __call__(self, op, buf):
+        import torch
+        import torch.distributed as dist
+
+        from . import _native as N
         if op == N.COLL_BCAST0:
-            dist.broadcast(t, src=0, group=group)
+            dist.broadcast(torch.from_numpy(buf), src=0, group=self.group)
             return
         if op != N.COLL_SUM:
             raise ValueError(f"collective op {op}")
-        parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
-        dist.all_gather(parts, t, group=group)
-        s = torch.zeros_like(t)
-        for p in parts:
-            s += p
-        t.copy_(s)
-    return run
+        self._sum(buf, True)
+
+    def fail_pending(self, n_floats):
+        """join the merge collective the peers wait in, flag cleared"""
+        import numpy as _np
+        try:
+            self._sum(_np.zeros(int(n_floats), _np.float32), False)
+        except PeerFailed:
+            pass
+
+
+def host_collective(group=None):
+    return HostCollective(group)
+
+
+def merge_floats(engine, rule):
+    """floats one libg2v merge all-reduces (g2v_api.hip merge_now): both
+    tables, then touched counts (and squared norms for align)"""
+    tab = int(engine.V) * int(engine.ld)
+    return 2 * tab + {"mean": 0, "touch": 2, "align": 4}[rule] * int(engine.V)
 
 
 def world_size(group=None):
@@ -338,6 +384,8 @@ class ReplicaTrainer:
             own = (n_jobs + every - 1) // every
             self.engine.set_option(N.OPT_MERGE_RULE, MERGE_RULES[self.merge])
             self.engine.set_option(N.OPT_MERGE_EVERY_JOBS, every)
+            hc = getattr(self.engine, "host_collective", None)
+            sums0 = hc.sums if isinstance(hc, HostCollective) else None
             err = None
             try:
                 if n_jobs > 0:
@@ -346,6 +394,13 @@ class ReplicaTrainer:
                     self.engine.average(MERGE_RULES[self.merge])
             except Exception as e:  # libg2v already left the communicator
                 err = e
+                # host transport: peers block inside their next merge's gather;
+                # join it with the ok flag cleared so they fail out of it (a peer
+                # itself failing there also fails, and joins nothing more)
+                if (sums0 is not None and not isinstance(e, PeerFailed)
+                        and not isinstance(getattr(e, "__cause__", None), PeerFailed)
+                        and hc.sums - sums0 < n_win):
+                    hc.fail_pending(merge_floats(self.engine, self.merge))
             finally:
                 # later train() calls of this engine (not data-parallel) merge nothing
                 self.engine.set_option(N.OPT_MERGE_EVERY_JOBS, 0)

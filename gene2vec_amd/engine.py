@@ -269,6 +269,7 @@ class SGNSEngine:
         return bytes(buf)
 
     def comm_init(self, unique_id, nranks, rank):
+        self.host_collective = None
         buf = (C.c_char * N.UNIQUE_ID_BYTES).from_buffer_copy(unique_id)
         N.check(self._lib.g2v_comm_init(self._h, buf, nranks, rank))
 
@@ -303,6 +304,8 @@ class SGNSEngine:
                 return 1
         self._coll_error = None
         self._coll_fn = N.COLLECTIVE_FN(tramp)  # kept alive with the engine
+        # ReplicaTrainer's failure protocol reads it (distributed.HostCollective)
+        self.host_collective = collective
         self._check_coll(self._lib.g2v_comm_init_host(self._h, self._coll_fn, None, nranks, rank))
 
     def _check_coll(self, rc):

@@ -161,7 +161,12 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_ACTIVE_WAVES  Hogwild kernel: waves per workgroup that train, 1..4;
  *                         with G2V_OPT_GRID 1 and 1 wave the production kernel
  *                         runs its chunks in record order, a deterministic
- *                         update order (parity checks) [4] */
+ *                         update order (parity checks) [4]
+ *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the
+ *                         n-th in-call merge of every g2v_train call fails
+ *                         before its collective, as a rank that dies between
+ *                         two merges would (g2v_train then leaves the
+ *                         communicator); 0 = off [0] */
 #define G2V_OPT_HOT_ROWS 1
 #define G2V_OPT_CACHE_POLICY 2
 #define G2V_OPT_SEG_JOBS 3
@@ -179,10 +184,12 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_ACTIVE_WAVES 15
 #define G2V_OPT_MERGE_BETA_MILLI 16
 #define G2V_OPT_MERGE_GAMMA_MILLI 17
+#define G2V_OPT_DEBUG_FAIL_MERGE 18
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
-/* Current value of an option (G2V_OPT_GRID: the workgroups the next Hogwild
- * launch uses -- by default 2 per CU, fewer for vocabularies whose hottest
- * row takes more updates per example than C4's, see g2v_set_vocab). */
+/* Current value of an option (G2V_OPT_GRID: the workgroups g2v_set_vocab
+ * chose -- by default the staleness budget's, at most one per CU; a Hogwild
+ * g2v_train call may lower it further (the per-call stability cap), and
+ * g2v_read_stats reports the grid and stripe layout the last launch used). */
 int g2v_get_option(g2v_ctx *ctx, int key, int64_t *value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);

@@ -87,8 +87,6 @@ def main():
             eng.set_option(N.OPT_DEBUG_WRITE, int(cfg["dbg"]))
         if "aw" in cfg:  # waves per workgroup that train (grid spreads them over more CUs)
             eng.set_option(N.OPT_ACTIVE_WAVES, int(cfg["aw"]))
-        if "drain" in cfg:  # drained stripe copies (profiles/r03/s4_drained_copy_variant.patch)
-            eng.set_option(18, int(cfg["drain"]))
         if "ov" in cfg:
             eng.set_option(N.OPT_ATOMIC_OVERLAP, int(cfg["ov"]))
         mode = N.MODE_SEQUENTIAL if cfg.get("mode") == "seq" else N.MODE_HOGWILD

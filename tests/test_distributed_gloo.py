@@ -52,6 +52,39 @@ class FailingEngine:
         self.aborted = True
 
 
+class HostMergingEngine:
+    """libg2v over the host transport, as ReplicaTrainer sees it: train() runs
+    one merge collective (Dd.HostCollective, flagged) at the end of every
+    window of OPT_MERGE_EVERY_JOBS jobs, as g2v_train's in-call merges do, and
+    fails before merge `fail_before` (1-based) like G2V_OPT_DEBUG_FAIL_MERGE"""
+
+    def __init__(self, fail_before=0, V=5, ld=4):
+        from gene2vec_amd import _native as N
+        self.N, self.V, self.ld, self.fail_before = N, V, ld, fail_before
+        self.opts, self.aborted = {}, False
+        self.host_collective = Dd.HostCollective()
+
+    def set_option(self, k, v):
+        self.opts[k] = v
+
+    def _merge(self):
+        buf = np.ones(Dd.merge_floats(self, "touch"), np.float32)
+        self.host_collective(self.N.COLL_SUM, buf)
+
+    def train(self, js, al, sd, mode, timing=False, compute_loss=False):
+        every = self.opts[self.N.OPT_MERGE_EVERY_JOBS]
+        for w in range((len(al) + every - 1) // every):
+            if w + 1 == self.fail_before:
+                raise RuntimeError("injected failure before in-call merge")
+            self._merge()
+
+    def average(self, rule):
+        self._merge()
+
+    def comm_abort(self):
+        self.aborted = True
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -146,6 +179,19 @@ def _worker(rank, world, port, q):
             out["fail"] = str(e)
         out["aborted"] = fe.aborted
         out["merge_every_reset"] = fe.opts.get(N.OPT_MERGE_EVERY_JOBS)
+        # host transport: rank 1 fails between its in-call merges while rank 0
+        # waits inside merge 2's gather; rank 1 joins that gather with its ok
+        # flag cleared, rank 0 fails out of it, and both agree (no mismatched
+        # gloo collectives, no hang: the agreements below still line up)
+        he = HostMergingEngine(fail_before=2 if rank == 1 else 0)
+        tr4 = Dd.ReplicaTrainer(he, (), avg_every_jobs=4, backend="libg2v")
+        try:
+            tr4.train_epoch(np.arange(0, 21, 2, dtype=np.int64), np.zeros(10),
+                            np.zeros(10, np.uint64))
+            out["host_fail"] = None
+        except Exception as e:
+            out["host_fail"] = f"{type(e).__name__}: {e}"
+        out["host_sums"] = he.host_collective.sums
         out["max_int"] = Dd.allreduce_max_int(5 + rank)
         out["sum_float"] = Dd.allreduce_sum_float(0.5 * (rank + 1))
         q.put((rank, out))
@@ -246,6 +292,16 @@ def test_libg2v_backend_failure_reaches_every_rank(results):
     assert "another rank" in results[0]["fail"] and results[0]["aborted"]
     for r in (0, 1):
         assert results[r]["merge_every_reset"] == 0
+
+
+def test_host_transport_failure_between_merges(results):
+    """the failing rank joins its peer's pending merge with
+    the ok flag cleared; the peer raises PeerFailed, the failing rank its own
+    error, and the later scalar agreement (max_int) still matches up"""
+    assert results[1]["host_fail"] == "RuntimeError: injected failure before in-call merge"
+    assert results[0]["host_fail"].startswith("PeerFailed: rank(s) [1] failed")
+    assert results[0]["host_sums"] == 1 and results[1]["host_sums"] == 1
+    assert results[0]["max_int"] == results[1]["max_int"] == 6
 
 
 def test_thread_agreement_min():
