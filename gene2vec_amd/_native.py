@@ -19,7 +19,7 @@ G2V_ENOMEM = -3
 G2V_ESTATE = -4
 G2V_ERANGE = -5
 G2V_ECOMM = -6
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
@@ -108,6 +108,7 @@ SIGNATURES = {
     "g2v_train": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _u32]),
     "g2v_sgns_step_explicit": (C.c_int, [_vp, _vp, _vp, _vp, _i64, _f32, _u32]),
     "g2v_debug_sample": (C.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, C.POINTER(_i64)]),
+    "g2v_debug_stamps": (C.c_int, [_vp, _vp, _i64]),
     "g2v_reset_loss": (C.c_int, [_vp]),
     "g2v_sync": (C.c_int, [_vp]),
     "g2v_comm_unique_id": (C.c_int, [_vp, _i64]),

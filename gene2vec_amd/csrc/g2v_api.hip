@@ -221,6 +221,7 @@ struct g2v_ctx {
   double* d_loss = nullptr;
   unsigned int* d_queue = nullptr;  // k_sgns_atomic work queue (one counter)
   unsigned int* d_norm = nullptr;   // stability_grid's max squared row norm (float bits)
+  unsigned long long* d_stamps = nullptr;  // G2V_OPT_DEBUG_WRITE 8: segment cycle sums
 
   // replica merge: snapshot of both tables at the last merge, touched-row counts
   float *merge0 = nullptr, *merge1 = nullptr, *merge_cnt = nullptr;
@@ -560,6 +561,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->d_loss);
   dev_free(c->d_queue);
   dev_free(c->d_norm);
+  dev_free(c->d_stamps);
   dev_free(c->merge0);
   dev_free(c->merge1);
   dev_free(c->merge_cnt);
@@ -648,7 +650,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 7, G2V_EINVAL, "debug write mode out of [0, 7]");
+      REQUIRE(value >= 0 && value <= 8, G2V_EINVAL, "debug write mode out of [0, 8]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_ATOMIC_OVERLAP:
@@ -1062,7 +1064,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.exp_table = c->exp_table;
   // 6: production writes, 7: scratch atomics (mode 4); both read main rows only
   s.debug_write = c->debug_write == 6 ? 0 : c->debug_write == 7 ? 4 : c->debug_write;
-  s.skip_copy_reads = c->debug_write >= 6 ? 1 : 0;
+  s.skip_copy_reads = (c->debug_write == 6 || c->debug_write == 7) ? 1 : 0;
   s.compute_loss = closs ? 1 : 0;
   s.log_table = c->log_table;
   s.loss_f64 = c->d_loss;
@@ -1092,7 +1094,8 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   const int64_t max_rows2 = kStripeMaxBytes / (2 * 4 * (int64_t)(c->stripe2_copies - 1) * c->ld);
   const int r2 = (int)std::min<int64_t>(std::min(stripe2_rows_eff(c), c->V),
                                         (int64_t)s.stripe_rows + max_rows2);
-  const bool tier2 = striped && (c->debug_write == 0 || c->debug_write == 6) && r2 > s.stripe_rows;
+  const bool tier2 = striped && (c->debug_write == 0 || c->debug_write == 6 || c->debug_write == 8) &&
+                     r2 > s.stripe_rows;
   s.stripe2_rows = tier2 ? r2 : s.stripe_rows;
   s.stripe2_copies = tier2 ? c->stripe2_copies : 1;
   if (tier2) {
@@ -1110,6 +1113,11 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
   }
   s.dbg16 = c->dbg16;
+  if (c->debug_write == 8 && !c->d_stamps) {
+    if ((rc = dev_alloc(&c->d_stamps, kStampWords))) return rc;
+    HIPCHK(hipMemsetAsync(c->d_stamps, 0, kStampWords * sizeof(unsigned long long), c->stream));
+  }
+  s.stamps = c->d_stamps;
   if (atomic_kernel) HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(unsigned int), c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timing) {
@@ -1502,6 +1510,18 @@ int g2v_sync(g2v_ctx* c) {
   if (rc) return rc;
   HIPCHK(hipStreamSynchronize(c->stream));
   return check_fault(c);
+}
+
+int g2v_debug_stamps(g2v_ctx* c, uint64_t* out, int64_t n) {
+  int rc = set_dev(c);
+  if (rc) return rc;
+  REQUIRE(out != nullptr && n >= kStampWords, G2V_EINVAL, "need %d output words", kStampWords);
+  HIPCHK(hipStreamSynchronize(c->stream));
+  memset(out, 0, sizeof(uint64_t) * (size_t)n);
+  if (!c->d_stamps) return G2V_OK;
+  HIPCHK(hipMemcpy(out, c->d_stamps, kStampWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  HIPCHK(hipMemset(c->d_stamps, 0, kStampWords * sizeof(unsigned long long)));
+  return G2V_OK;
 }
 
 int g2v_reset_loss(g2v_ctx* c) {

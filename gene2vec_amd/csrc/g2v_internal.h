@@ -76,6 +76,8 @@ struct SampleArgs {
 constexpr unsigned long long kFaultTokenRange = 1;  // corpus id outside [-1, V)
 constexpr unsigned long long kFaultJobSize = 2;     // multi-sentence job > kBatchWords raw words
 
+constexpr int kStampWords = 16;  // g2v_debug_stamps: segment sums, counts, clocks
+
 struct SgnsArgs {
   const int32_t* rec;       // [E][rec_stride]: center, input, alpha bits, negs[K]
   int rec_stride;
@@ -108,6 +110,7 @@ struct SgnsArgs {
   int active_waves;         // G2V_OPT_ACTIVE_WAVES: waves per workgroup that train (1..4)
   unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]
+  unsigned long long* stamps;  // debug_write 8: per-segment cycle sums (g2v_debug_stamps)
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])

@@ -171,7 +171,8 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // 2 no table writes, 3 packed-f16 atomics into a scratch table (half the atomic
 // bytes, tables never written: a throughput probe), 4 the production f32
 // atomics into that scratch table (tables never written), 5 production atomics
-// on syn1neg only, syn0 never written (the ceiling of any syn0-side combining)
+// on syn1neg only, syn0 never written (the ceiling of any syn0-side combining),
+// 8 production with s_memtime stamps per loop segment (diagnostic build)
 //
 // One row's delta coef * src[0, D) as a FIXED 4 * NV wave-instructions: the
 // buffer resource spans the row's D floats, so lanes past D (and every lane of
@@ -194,7 +195,7 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
   for (int i = 0; i < 4 * NV; ++i) {
     const int off = (64 * i + lane) * 4;
     const float v = coef * src[i];
-    if (WR == 0 || WR == 4 || WR == 5)
+    if (WR == 0 || WR == 4 || WR == 5 || WR == 8)
       __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
     else if (WR == 1)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
@@ -218,6 +219,27 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 __device__ __forceinline__ float uniform_f(float x) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
 }
+
+// In-kernel stamps (WR 8 only; cdna_hip_programming.md 7 "In-kernel stamps"):
+// one asm statement per stamp, the lgkmcnt(0) inside it, fenced from the
+// scheduler on both sides.  Read the segment SHARES of such a build, never its
+// run time (the fences forbid overlaps the production kernel has).
+__device__ __forceinline__ uint64_t stamp_time() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+__device__ __forceinline__ uint64_t stamp_realtime() {
+  uint64_t t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+// s_waitcnt immediate (gfx9 layout) for vmcnt(n), lgkmcnt / expcnt not waited
+constexpr int waitcnt_vm(int n) { return 0x0F70 | (n & 0xF) | (((n >> 4) & 3) << 14); }
 
 __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
   unsigned int v = 0;
@@ -270,6 +292,14 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   for (int v = 0; v < NV; ++v)
     loff[v] = (lane + 64 * v) < a.nvec ? (uint32_t)(lane * 16 + 1024 * v) : kLaneOob;
 
+  // WR 8: cycle sums per segment (see g2v_debug_stamps), wave-uniform scalars
+  constexpr int kAtomicsPerExample = 4 * NV * (NT + 1);  // emit_row's fixed count
+  uint64_t acc[5] = {0, 0, 0, 0, 0};
+  uint64_t n_ex = 0, tl0 = 0, rl0 = 0;
+  if (WR == 8) {
+    rl0 = stamp_realtime();
+    tl0 = stamp_time();
+  }
   for (int64_t c = next_chunk(a.queue, lane); c * kChunk < E; c = next_chunk(a.queue, lane)) {
     const int64_t e_beg = c * kChunk;
     const int64_t e_end = (e_beg + kChunk < E) ? e_beg + kChunk : E;
@@ -296,6 +326,15 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
     for (int64_t e = e_beg; e < e_end; ++e) {
       const int q = (int)(e - e_beg);
       if (!a.overlap) __builtin_amdgcn_s_waitcnt(0x0F70);  // e-1's atomics land first
+      uint64_t ts = 0;
+      if (WR == 8) {
+        // the wait production makes at its first use of e's rows, made explicit
+        const uint64_t t0 = stamp_time();
+        __builtin_amdgcn_s_waitcnt(waitcnt_vm(kAtomicsPerExample));
+        ts = stamp_time();
+        acc[0] += ts - t0;
+        ++n_ex;
+      }
       // ---- compute example e ------------------------------------------------
       double pd[NT], dot[NT];
 #pragma unroll
@@ -395,6 +434,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       for (int d = 0; d < NT; ++d) tg[d] = x.tg[d];
       const int32_t input = x.input;
       const float lf = slf[q];
+      if (WR == 8) {
+        const uint64_t t = stamp_time();
+        acc[1] += t - ts;
+        ts = t;
+      }
 
       // ---- prefetch example e+1 (its loads overtake e's atomics) -------------
       // e-1's atomics retired behind e's compute; they must have landed before
@@ -402,7 +446,17 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       // before this pipelining: the Hogwild staleness stays what the grid
       // budget was measured with)
       __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      if (WR == 8) {
+        const uint64_t t = stamp_time();
+        acc[2] += t - ts;
+        ts = t;
+      }
       if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff);
+      if (WR == 8) {
+        const uint64_t t = stamp_time();
+        acc[3] += t - ts;
+        ts = t;
+      }
 
       // ---- atomics of example e -----------------------------------------------
       if (WR == 3) {
@@ -441,9 +495,23 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       emit_row<NV, WR>(upd_row<WR>(a, 0, input, cbase + NT, rowb),
                        any && WR != 5, D, vw, lf, lane);
       __builtin_amdgcn_wave_barrier();
+      if (WR == 8) acc[4] += stamp_time() - ts;
       cbase = cbase + 1 == a.stripe_copies ? 0 : cbase + 1;
     }
     if (LOSS && lane == 0 && lsum != 0.f) atomicAdd(a.loss_f64, (double)lsum);
+  }
+  if (WR == 8) {
+    const uint64_t tl = stamp_time() - tl0;
+    const uint64_t rl = stamp_realtime() - rl0;
+    if (lane == 0) {
+      unsigned long long* o = a.stamps;
+      for (int i = 0; i < 5; ++i) atomicAdd(o + i, (unsigned long long)acc[i]);
+      atomicAdd(o + 5, (unsigned long long)tl);
+      atomicAdd(o + 6, (unsigned long long)n_ex);
+      atomicAdd(o + 7, (unsigned long long)tl);
+      atomicAdd(o + 8, (unsigned long long)rl);
+      atomicAdd(o + 9, 1ull);
+    }
   }
 }
 
@@ -476,6 +544,10 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 3) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 3>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 8) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
 #endif

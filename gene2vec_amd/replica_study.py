@@ -223,6 +223,10 @@ class Study:
         self.ho_c, self.ho_j = hc[keep], hj[keep]
 
     def gmt(self, path):
+        if self.modules and self.V0 / self.modules > 50:
+            # src/evaluation_target_function.py:8-14 drops pathways of > 50 genes
+            raise ValueError(f"{self.V0} genes in {self.modules} modules: > 50 genes per module, "
+                             "every pathway would be dropped by the target function")
         if self.modules:
             module_gmt(path, module_of(self.V0, self.modules), self.modules, self.names)
         else:

@@ -330,7 +330,9 @@ class Word2Vec:
     gensim workers=1 order, for parity checks); ``data_parallel`` = True
     shards the corpus over an initialised torch.distributed group and merges
     the replicas (opt-in: the gene2vec CLI sets it under torchrun; a model
-    trained inside some unrelated process group stays single-GPU).
+    trained inside some unrelated process group stays single-GPU); ``grid``
+    fixes the Hogwild kernel's workgroups (G2V_OPT_GRID; 0 = the library's
+    staleness-bounded default with its per-call stability cap).
     ``compute_loss`` follows gensim 3.4: the running loss of the latest
     train() call, ``get_latest_training_loss()``."""
 
@@ -338,7 +340,8 @@ class Word2Vec:
                  max_vocab_size=None, sample=1e-3, seed=1, workers=3, min_alpha=0.0001,
                  sg=0, hs=0, negative=5, cbow_mean=1, hashfxn=hash, iter=5, null_word=0,
                  trim_rule=None, sorted_vocab=1, batch_words=N.BATCH_WORDS, compute_loss=False,
-                 callbacks=(), ns_exponent=0.75, device=0, mode="hogwild", data_parallel=False):
+                 callbacks=(), ns_exponent=0.75, device=0, mode="hogwild", data_parallel=False,
+                 grid=0):
         if sg != 1:
             raise NotImplementedError("only skip-gram (sg=1) is implemented (src/gene2vec.py:60)")
         if hs:
@@ -375,6 +378,7 @@ class Word2Vec:
         self.device = device
         self.mode = mode
         self.data_parallel = data_parallel
+        self.grid = int(grid)
         self.merge_every_jobs = DP_MERGE_EVERY_JOBS
         self.random = np.random.RandomState(seed)
         self.corpus_count = 0
@@ -514,6 +518,8 @@ class Word2Vec:
                                      dtype=np.uint64), 2 ** 32 - 1).astype(np.uint32)
         if not np.array_equal(si, expect):
             raise RuntimeError("device sample_int differs from the host vocabulary")
+        if getattr(self, "grid", 0):
+            eng.set_option(N.OPT_GRID, self.grid)
         eng.set_weights(wv.vectors, self.syn1neg, self.vectors_lockf)
         self._replica = None
         if self._dp_world()[1] > 1:
@@ -726,6 +732,7 @@ class Word2Vec:
         m.callbacks = ()
         m.device = 0
         m.data_parallel = False
+        m.grid = 0
         m.merge_every_jobs = DP_MERGE_EVERY_JOBS
         m.total_train_time = 0.0
         m.running_training_loss = float(meta.get("running_training_loss", 0.0))

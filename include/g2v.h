@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define G2V_ABI_VERSION 3
+#define G2V_ABI_VERSION 4
 
 /* status codes */
 #define G2V_OK 0
@@ -127,7 +127,10 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         atomics into a scratch table, 5 syn1neg atomics only
  *                         (syn0 never written), 6 stripe copies written but
  *                         never read (readers see main rows only), 7 = 4 with
- *                         main-row-only reads [0]
+ *                         main-row-only reads, 8 = the production kernel with
+ *                         s_memtime stamps per loop segment (diagnostic build,
+ *                         K 5 / D <= 256: g2v_debug_stamps; its run time is
+ *                         not a measurement, its segment SHARES are) [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE2_ROWS  second stripe tier: rows [STRIPE_ROWS, this) get
  *                         STRIPE2_COPIES copies each (<= STRIPE_ROWS = off);
@@ -274,6 +277,17 @@ int g2v_reset_loss(g2v_ctx *ctx);
  * rec_out[cap][K+2] in gensim order; *n_out = record count.  Synchronises. */
 int g2v_debug_sample(g2v_ctx *ctx, const int64_t *job_sent, const uint64_t *job_seed,
                      int64_t n_jobs, int32_t *rec_out, int64_t cap, int64_t *n_out);
+
+/* Diagnostic (G2V_OPT_DEBUG_WRITE 8): shader-cycle sums of the stamped
+ * Hogwild kernel over every wave of every launch since the previous call
+ * (synchronises, then resets): out[0] waiting for the example's rows, [1]
+ * compute (dots, sigmoid, gradients, LDS staging), [2] waiting for the
+ * previous example's atomics to land, [3] issuing the next example's loads
+ * (incl. summing striped rows' copies), [4] issuing this example's atomics,
+ * [5] whole loop per wave (the rest is per-chunk work: record staging, the
+ * work queue), [6] examples, [7] s_memtime ticks and [8] s_memrealtime ticks
+ * (100 MHz) over the loops (clock = [7] / [8] x 100 MHz), [9] waves; n >= 10. */
+int g2v_debug_stamps(g2v_ctx *ctx, uint64_t *out, int64_t n);
 
 /* ---- sync / stats ------------------------------------------------------------ */
 /* Synchronises the context's stream; reports (and clears) a latched device

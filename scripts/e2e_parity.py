@@ -12,7 +12,7 @@ sawtooth restarting at every train() call, per-job seeds from model.random,
 compute_loss on the last iteration.
 
 Corpus: Zipf(1) gene pairs over --vocab genes with --modules planted
-co-expression modules (scripts/replica_quality.planted_pairs: half the pairs
+co-expression modules (gene2vec_amd/replica_study.planted_pairs: half the pairs
 rewired inside the first gene's module) plus the reference's GGIPNN positive
 pairs (data/predictionData, all three splits, label-leaky as in
 scripts/ggipnn_e2e.py) repeated --ggipnn-repeat times.
@@ -40,10 +40,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
-import replica_quality as RQ  # noqa: E402
 from gene2vec_amd import _native as N  # noqa: E402
+from gene2vec_amd import replica_study as RQ  # noqa: E402
 from gene2vec_amd import engine as E  # noqa: E402
 from gene2vec_amd import synthetic as S  # noqa: E402
 from oracle import c_oracle as CO  # noqa: E402
@@ -180,9 +179,13 @@ def main():
             tr = time.time() - t
             res = {"train_s": round(tr, 1), **extra,
                    "heldin": round(RQ.heldin(s0, s1, tok0, vc, K), 5)}
-            res.update(RQ.export_and_score(f"{eng_name}{seed}", s0, index2word, vc, pos_genes,
-                                           gmt, a.out,
-                                           [int(x) for x in a.auc_seeds.split(",") if x], D))
+            t = RQ.target_of(s0, index2word, vc, gmt, D)
+            res.update({"target_ratio": t["ratio"], "path_mean": t["path_mean"],
+                        "rand_mean": t["rand_mean"], "n_pathways": t["n_pathways"]})
+            auc_seeds = [int(x) for x in a.auc_seeds.split(",") if x]
+            if auc_seeds:
+                aucs = RQ.ggipnn_auc(s0, index2word, pos_genes, auc_seeds)
+                res.update({"auc": aucs, "auc_mean": float(np.mean(aucs))})
             log["runs"][f"{eng_name}_seed{seed}"] = res
             print(eng_name, seed, json.dumps(res), flush=True)
             json.dump(log, open(os.path.join(a.out, "e2e_parity.json"), "w"), indent=1)

@@ -23,7 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "scripts"))
 from gene2vec_amd import engine as E  # noqa: E402
 from gene2vec_amd import synthetic as S  # noqa: E402
 from oracle import c_oracle as CO  # noqa: E402
-import replica_quality as RQ  # noqa: E402
+from gene2vec_amd import replica_study as RQ  # noqa: E402
 
 
 def merge(rule, ts, olds, beta=1.0, gamma=1.0):

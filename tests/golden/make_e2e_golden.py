@@ -3,6 +3,8 @@
 after the reference's 10-iteration flow on tests.helpers.e2e_corpus().
 
     python tests/golden/make_e2e_golden.py     # ~2 minutes on one CPU
+    python tests/golden/make_e2e_golden.py --v5k   # e2e_parity_v5k.json
+    python tests/golden/make_e2e_golden.py --c2    # e2e_parity_c2.json
 
 Per model.random seed: the last iteration's training loss (gensim's
 compute_loss terms summed in double), the SGNS objective on 40,000 corpus
@@ -23,7 +25,7 @@ sys.path.insert(0, ROOT)
 from gene2vec_amd import engine as E  # noqa: E402
 from oracle import c_oracle as CO  # noqa: E402
 from oracle import target_oracle as TO  # noqa: E402
-from tests.helpers import E2E, E2E_C2, e2e_corpus, e2e_heldin  # noqa: E402
+from tests.helpers import E2E, E2E_C2, E2E_V5K, e2e_corpus, e2e_heldin  # noqa: E402
 
 
 def main(cfg=E2E, out_name="e2e_parity.json", with_sample0=True):
@@ -73,5 +75,7 @@ def main(cfg=E2E, out_name="e2e_parity.json", with_sample0=True):
 if __name__ == "__main__":
     if "--c2" in sys.argv:  # the C2 vocabulary: ~5 minutes per seed
         main(E2E_C2, "e2e_parity_c2.json", with_sample0=False)
+    elif "--v5k" in sys.argv:  # the dense 5,000-gene corpus: ~1 minute per seed
+        main(E2E_V5K, "e2e_parity_v5k.json", with_sample0=False)
     else:
         main()

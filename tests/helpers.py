@@ -124,6 +124,11 @@ E2E = {"V0": 3000, "modules": 100, "p_in": 0.5, "pairs": 2_000_000, "iters": 10,
 # the same flow at the C2 bench vocabulary (tests/golden/e2e_parity_c2.json)
 E2E_C2 = dict(E2E, V0=24447, modules=1000, pairs=10_000_000, seeds=(1, 2))
 
+# a dense corpus (5,000 genes, 200 modules, 4 M pairs: every gene in ~1,600
+# pairs), where the Hogwild staleness moves the target function most
+# (tests/golden/e2e_parity_v5k.json)
+E2E_V5K = dict(E2E, V0=5000, modules=200, pairs=4_000_000, seeds=(1, 2, 3))
+
 
 def e2e_corpus(c=None):
     """(tok int32[2n] in vocab index order, vocab counts, index2word, pathway

@@ -74,18 +74,3 @@ def test_c3_eight_replicas_within_one_percent_of_one_model(tmp_path):
     for k, g in gaps.items():
         assert abs(g) < 0.01, (k, one, rep)
 
-
-def test_cli_defaults_match_the_c3_gate():
-    """(CPU) the gate above runs the CLI's defaults: a merge every 4,096 jobs
-    and sharding from 125 M pairs per rank"""
-    from unittest import mock
-
-    from gene2vec_amd import gene2vec as G
-    seen = {}
-
-    def fake_init(args):
-        seen.update(vars(args))
-        raise SystemExit(0)
-    with mock.patch.object(G, "_init_dp", fake_init), pytest.raises(SystemExit):
-        G.main(["d", "o", "txt"])
-    assert seen["merge_every_jobs"] == 4096 and seen["dp_min_pairs_per_rank"] == 125_000_000

@@ -27,7 +27,7 @@ from gene2vec_amd import engine as E
 from gene2vec_amd import evaluate as EV
 from gene2vec_amd.word2vec import KeyedVectors, Vocab
 from tests.conftest import GOLDEN
-from tests.helpers import E2E, E2E_C2, e2e_corpus, e2e_heldin
+from tests.helpers import E2E, E2E_C2, E2E_V5K, e2e_corpus, e2e_heldin
 
 pytestmark = pytest.mark.gpu
 
@@ -127,6 +127,23 @@ def test_gpu_end_to_end_at_the_c2_vocabulary(tmp_path):
     got = _train_e2e(tmp_path, E2E_C2["sample"], cfg=E2E_C2)
     gaps = _gaps(got, ref)
     print("gpu C2 vocabulary", got, "gaps vs sequential oracle", gaps)
+    assert abs(gaps["loss"]) < 0.01, gaps
+    assert abs(gaps["heldin"]) < 0.005, gaps
+    assert abs(gaps["target_ratio"]) < 0.01, gaps
+
+
+def test_gpu_end_to_end_dense_5k_genes(tmp_path):
+    """the dense corpus where Hogwild staleness moves the target function most
+    (5,000 genes, 200 planted modules, 4 M pairs: every gene in ~1,600 pairs;
+    DESIGN.md 8 measured -0.97 % at the default one-workgroup-per-CU grid with
+    GGIPNN pairs added, -1.39 % at the 295 workgroups the staleness budget
+    alone allowed).  Golden: the sequential oracle, three seeds
+    (tests/golden/make_e2e_golden.py --v5k).  North-star bar: 1 % on the loss
+    and the target function, 0.5 % on the SGNS objective."""
+    ref = _golden("e2e_parity_v5k.json", E2E_V5K)
+    got = _train_e2e(tmp_path, E2E_V5K["sample"], cfg=E2E_V5K)
+    gaps = _gaps(got, ref)
+    print("gpu dense 5k genes", got, "gaps vs sequential oracle", gaps)
     assert abs(gaps["loss"]) < 0.01, gaps
     assert abs(gaps["heldin"]) < 0.005, gaps
     assert abs(gaps["target_ratio"]) < 0.01, gaps
