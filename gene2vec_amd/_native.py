@@ -74,7 +74,8 @@ class Stats(C.Structure):
                 ("sgns_kernel_ms", C.c_double), ("sample_kernel_ms", C.c_double),
                 ("training_loss", C.c_double), ("sgns_grid", C.c_int64),
                 ("stripe_rows", C.c_int64), ("stripe_copies", C.c_int64),
-                ("stripe2_rows", C.c_int64), ("stripe2_copies", C.c_int64)]
+                ("stripe2_rows", C.c_int64), ("stripe2_copies", C.c_int64),
+                ("sgns_waves", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -139,7 +139,6 @@ struct g2v_ctx {
   bool grid_user = false;       // G2V_OPT_GRID set explicitly
   double u_max = 0.0;           // hottest row's updates per example (set_vocab)
   double p_tok_max = 0.0;       // hottest row's share of the kept tokens (syn0 input rate)
-  int call_grid = 0;            // this g2v_train call's Hogwild grid (0: sgns_grid)
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
@@ -220,7 +219,8 @@ struct g2v_ctx {
   float* log_table = nullptr;
   double* d_loss = nullptr;
   unsigned int* d_queue = nullptr;  // k_sgns_atomic work queue (one counter)
-  unsigned int* d_norm = nullptr;   // stability_grid's max squared row norm (float bits)
+  unsigned int* d_norm = nullptr;   // the stability cap's max squared row norm (float bits)
+  int* d_waves = nullptr;           // waves that trained in the last Hogwild launch
   unsigned long long* d_stamps = nullptr;  // G2V_OPT_DEBUG_WRITE 8: segment cycle sums
 
   // replica merge: snapshot of both tables at the last merge, touched-row counts
@@ -262,6 +262,24 @@ struct g2v_ctx {
 // quiet end: waves x u_max <= 125 (C2 256 workgroups, C4 117, V 3,000 149).
 constexpr double kStaleBudget = 125.0;
 
+// Stability cap of the Hogwild waves (k_sgns_atomic, evaluated on the device
+// before every launch).  The staleness budget above bounds the in-flight
+// updates of the hottest syn1neg row; a hot syn0 row is the other risk: its
+// delta sums K+1 terms g * syn1neg[t], so its in-flight updates overshoot once
+// waves x p_tok x (K+1) x alpha x |syn1neg|^2 grows, which it does as
+// training structures the vectors.  Measured, |syn1neg|^2 the
+// largest squared row norm of syn1neg (a hot input's centres are any rows): a
+// 3,000-gene corpus with planted modules at sample 0 diverged at a later
+// sawtooth restart with 163 and 137 workgroups (a hot syn0 row's |v|^2 jumping
+// 14 -> 90-215 and frozen there by the |f| >= 6 skip; products 190-250) and
+// trained to the sequential order's objective at 64 (product 90); the C2 / C4
+// vocabularies at sample 1e-3 and pure Zipf at sample 0 stay below the cap at
+// their default grids.  So the waves that train are capped where the product,
+// from |syn1neg|^2 just before the launch and the launch's largest alpha,
+// reaches 100 (round 3 evaluated it once per g2v_train call, from a host
+// read-back; a whole data-parallel epoch in one call was never re-capped).
+constexpr double kSyn0Budget = 100.0;
+
 // Copies per striped hot row when G2V_OPT_STRIPE_COPIES is not set.  Every
 // read of a striped row sums its copies (one more load batch on the example's
 // critical path); every copy spreads that row's atomics.  At one workgroup per
@@ -269,9 +287,9 @@ constexpr double kStaleBudget = 125.0;
 // (C2 266 WGs: 202.6 M ex/s vs 197.2 with 8); below, the grid is held down by
 // the staleness budget, per-example latency binds and 8 win (C2 sample 0 at
 // 162 WGs: 153.6 vs 136.4; C4 at 121: 36.8 vs 36.1).
-// the Hogwild grid of the launches being issued: the call's stability cap
-// (train_impl) or the context's grid
-static int launch_grid(const g2v_ctx* c) { return c->call_grid > 0 ? c->call_grid : c->sgns_grid; }
+// the Hogwild grid of the launches being issued (the stability cap, DESIGN.md
+// 5c, lowers the waves that train inside a launch, not the grid)
+static int launch_grid(const g2v_ctx* c) { return c->sgns_grid; }
 
 static int stripe_copies_eff(const g2v_ctx* c) {
   if (c->stripe_copies > 0) return c->stripe_copies;
@@ -490,7 +508,7 @@ int g2v_create(int device, int32_t vocab_size, int32_t vector_size, int32_t nega
       (rc = dev_alloc(&c->d_counts, (size_t)c->V)) || (rc = dev_alloc(&c->d_cpow, (size_t)c->V)) ||
       (rc = dev_alloc(&c->d_counters, 4)) || (rc = dev_alloc(&c->log_table, kExpTableSize)) ||
       (rc = dev_alloc(&c->d_loss, 2)) || (rc = dev_alloc(&c->d_queue, 1)) ||
-      (rc = dev_alloc(&c->d_norm, 1)))
+      (rc = dev_alloc(&c->d_norm, 1)) || (rc = dev_alloc(&c->d_waves, 1)))
     return bail(rc);
   c->syn0 = c->own0;
   c->syn1 = c->own1;
@@ -561,6 +579,7 @@ int g2v_destroy(g2v_ctx* c) {
   dev_free(c->d_loss);
   dev_free(c->d_queue);
   dev_free(c->d_norm);
+  dev_free(c->d_waves);
   dev_free(c->d_stamps);
   dev_free(c->merge0);
   dev_free(c->merge1);
@@ -1044,9 +1063,11 @@ static int sample_segment(g2v_ctx* c, int64_t j0, int64_t nj, bool timing, int b
   return G2V_OK;
 }
 
+// amax: the launch's largest alpha, for the stability cap of a Hogwild
+// launch on the library's grid (0: no cap)
 static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool timing,
                     bool closs, const float* rd0, const float* rd1,
-                    const int32_t* rec = nullptr) {
+                    const int32_t* rec = nullptr, float amax = 0.f) {
   SgnsArgs s{};
   s.rec = rec ? rec : c->d_rec;
   s.rec_stride = c->rec_stride;
@@ -1118,6 +1139,17 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipMemsetAsync(c->d_stamps, 0, kStampWords * sizeof(unsigned long long), c->stream));
   }
   s.stamps = c->d_stamps;
+  s.waves_out = atomic_kernel ? c->d_waves : nullptr;
+  if (atomic_kernel && amax > 0.f && !c->grid_user) {
+    // the cap from the tables as they are now (every launch: a single long
+    // call -- a data-parallel epoch -- is re-capped as the norms grow), with
+    // no host synchronisation; 33 us at C2 per ~28 ms launch
+    HIPCHK(hipMemsetAsync(c->d_norm, 0, sizeof(unsigned int), c->stream));
+    HIPCHK(launch_row_norm2_max(c->syn1, c->V, c->ld, c->D, c->d_norm, c->stream));
+    s.norm_bits = c->d_norm;
+    s.cap_coef = (float)(c->p_tok_max * (c->K + 1) * (double)amax);
+    s.cap_budget = (float)kSyn0Budget;
+  }
   if (atomic_kernel) HIPCHK(hipMemsetAsync(c->d_queue, 0, sizeof(unsigned int), c->stream));
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (timing) {
@@ -1233,42 +1265,6 @@ int g2v_train(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha, const
 
 }  // extern "C"
 
-// Stability cap of the Hogwild grid for one g2v_train call.  The staleness
-// budget of default_grid bounds the in-flight updates of the hottest syn1neg
-// row; a hot syn0 row is the other risk: its delta sums K+1 terms g * syn1neg[t],
-// so in-flight updates to it overshoot once waves x p_tok x (K+1) x alpha x
-// |syn1neg|^2 grows, which it does as training structures the vectors.
-// Measured, with |syn1neg|^2 the largest squared row norm of
-// syn1neg (a hot input's centres are any rows): a 3,000-gene corpus with
-// planted modules at sample 0 diverged at a later sawtooth restart with 163
-// and 137 workgroups (a hot syn0 row's |v|^2 jumping 14 -> 90-215 and frozen
-// there by the |f| >= 6 skip; products 190-250) and trained to the
-// sequential order's objective at 64 (product 90); the other corpora measured
-// (C2 / C4 vocabularies, sample 1e-3, and pure Zipf at sample 0) stay below
-// the cap at their default grids.  So the call's grid is capped where the
-// product, from |syn1neg|^2 at the call's start and the call's largest alpha,
-// reaches 100.
-constexpr double kSyn0Budget = 100.0;
-
-static int stability_grid(g2v_ctx* c, const float* job_alpha, int64_t n_jobs) {
-  double amax = 0.0;
-  for (int64_t j = 0; j < n_jobs; ++j) amax = std::max(amax, (double)job_alpha[j]);
-  unsigned int bits = 0;
-  HIPCHK(hipMemsetAsync(c->d_norm, 0, sizeof(unsigned int), c->stream));
-  HIPCHK(launch_row_norm2_max(c->syn1, c->V, c->ld, c->D, c->d_norm, c->stream));
-  HIPCHK(hipMemcpyAsync(&bits, c->d_norm, sizeof(unsigned int), hipMemcpyDeviceToHost, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  float k1f;
-  memcpy(&k1f, &bits, sizeof k1f);
-  const double k1 = (double)k1f;
-  const double per_wave = c->p_tok_max * (c->K + 1) * amax * k1;
-  if (per_wave <= 0.0) return G2V_OK;
-  const double waves = kSyn0Budget / per_wave;
-  if (waves >= (double)c->sgns_grid * c->active_waves) return G2V_OK;  // the default is within it
-  c->call_grid = (int)std::max(1.0, std::floor(waves / c->active_waves));
-  return G2V_OK;
-}
-
 static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alpha,
                       const uint64_t* job_seed, int64_t n_jobs, uint32_t flags) {
   int rc;
@@ -1282,13 +1278,6 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
   if (n_jobs == 0) return G2V_OK;
   const bool timing = flags & G2V_FLAG_TIMING;
   const bool closs = flags & G2V_FLAG_COMPUTE_LOSS;
-  c->call_grid = 0;
-  if (mode == kModeHogwild && !c->grid_user && (rc = stability_grid(c, job_alpha, n_jobs)))
-    return rc;
-  struct ResetCallGrid {
-    g2v_ctx* c;
-    ~ResetCallGrid() { c->call_grid = 0; }
-  } reset_call_grid{c};
   if ((rc = upload_jobs(c, job_sent, job_alpha, job_seed, n_jobs))) return rc;
   // segments of <= seg_jobs jobs; with G2V_OPT_MERGE_EVERY_JOBS and a
   // communicator, windows of merge_every jobs end with a replica merge
@@ -1297,6 +1286,7 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
   struct Seg {
     int64_t j0, nj;
     bool merge;
+    float amax;  // the segment's largest alpha (the stability cap)
   };
   std::vector<Seg> segs;
   const bool merging = c->comm_kind != kCommNone && c->merge_every > 0;
@@ -1305,7 +1295,10 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
     const int64_t w1 = std::min<int64_t>(n_jobs, w0 + win);
     for (int64_t j0 = w0; j0 < w1; j0 += c->seg_jobs) {
       const int64_t nj = std::min<int64_t>(c->seg_jobs, w1 - j0);
-      segs.push_back({j0, nj, merging && j0 + nj == w1});
+      float am = 0.f;
+      if (mode == kModeHogwild)
+        for (int64_t j = j0; j < j0 + nj; ++j) am = std::max(am, job_alpha[j]);
+      segs.push_back({j0, nj, merging && j0 + nj == w1, am});
     }
   }
   const int64_t n_seg = (int64_t)segs.size();
@@ -1319,7 +1312,8 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
   if (!c->sample_overlap || n_seg == 1) {
     for (const Seg& g : segs) {
       if ((rc = sample_segment(c, g.j0, g.nj, timing))) return rc;
-      if ((rc = run_sgns(c, c->d_job_exoff + g.nj, mode, timing, closs, c->syn0, c->syn1)))
+      if ((rc = run_sgns(c, c->d_job_exoff + g.nj, mode, timing, closs, c->syn0, c->syn1,
+                         nullptr, g.amax)))
         return rc;
       if (g.merge && (rc = merge())) return rc;
     }
@@ -1351,7 +1345,7 @@ static int train_impl(g2v_ctx* c, const int64_t* job_sent, const float* job_alph
     }
     HIPCHK(hipStreamWaitEvent(c->stream, c->ev_samp[b], 0));
     if ((rc = run_sgns(c, (b ? c->d_job_exoff2 : c->d_job_exoff) + g.nj, mode, timing, closs,
-                       c->syn0, c->syn1, b ? c->d_rec2 : c->d_rec)))
+                       c->syn0, c->syn1, b ? c->d_rec2 : c->d_rec, g.amax)))
       return rc;
     HIPCHK(hipEventRecord(c->ev_sgns[b], c->stream));
     if (g.merge && (rc = merge())) return rc;
@@ -1557,6 +1551,9 @@ int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
   out->stripe_copies = c->last_stripe_copies;
   out->stripe2_rows = c->last_stripe2_rows;
   out->stripe2_copies = c->last_stripe2_copies;
+  int waves = 0;
+  if (c->last_grid > 0) HIPCHK(hipMemcpy(&waves, c->d_waves, sizeof waves, hipMemcpyDeviceToHost));
+  out->sgns_waves = waves;
   for (auto& p : c->t_sgns) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));

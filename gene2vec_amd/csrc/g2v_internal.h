@@ -111,6 +111,14 @@ struct SgnsArgs {
   unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
   uint32_t* dbg16;          // ablation 3 only: packed-f16 scratch, [2][V + stripe rows][ld/2]
   unsigned long long* stamps;  // debug_write 8: per-segment cycle sums (g2v_debug_stamps)
+  // stability cap (k_sgns_atomic): waves that train =
+  // min(grid x active_waves, cap_budget / (cap_coef x max_r |syn1neg[r]|^2)),
+  // the norm read from *norm_bits (float bits) on the device, refreshed before
+  // every launch; norm_bits == nullptr: every wave trains
+  const unsigned int* norm_bits;
+  float cap_coef;           // p_tok_max x (K+1) x the launch's largest alpha
+  float cap_budget;
+  int* waves_out;           // the waves that trained (block 0 writes it)
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])

@@ -270,6 +270,22 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   // chunks train in record order and the update order is a fixed function of
   // the records, restated in oracle/sgns_oracle.c (oracle_atomic_one_wave)
   if (wid >= a.active_waves) return;
+  {
+    // stability cap: a hot syn0 row's in-flight updates scale
+    // with waves x p_tok x (K+1) x alpha x |syn1neg|^2; from the norm measured
+    // just before this launch, only the first `cap` waves (spread wave-major
+    // over the workgroups, so as many CUs as possible keep one) train
+    int cap = (int)gridDim.x * a.active_waves;
+    if (a.norm_bits != nullptr) {
+      const float per_wave = a.cap_coef * __uint_as_float(*a.norm_bits);
+      if (per_wave > 0.f) {
+        const float w = a.cap_budget / per_wave;
+        if (w < (float)cap) cap = w < 1.f ? 1 : (int)w;
+      }
+    }
+    if (a.waves_out != nullptr && blockIdx.x == 0 && wid == 0 && lane == 0) *a.waves_out = cap;
+    if (wid * (int)gridDim.x + (int)blockIdx.x >= cap) return;
+  }
   const int64_t E = *a.n_examples;
   const int D = a.D;
   const int64_t tbytes = (int64_t)a.V * a.ld * 4;

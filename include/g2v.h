@@ -88,6 +88,9 @@ typedef struct g2v_stats {
      * copies); the defaults are derived from the vocabulary at g2v_set_vocab */
     int64_t sgns_grid;
     int64_t stripe_rows, stripe_copies, stripe2_rows, stripe2_copies;
+    /* waves that trained in that launch (ABI 4): sgns_grid x the active waves,
+     * fewer where the stability cap held them back */
+    int64_t sgns_waves;
 } g2v_stats;
 
 /* ---- errors / version --------------------------------------------------- */
@@ -115,11 +118,12 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *   G2V_OPT_SEG_JOBS      gensim jobs per sampling/update segment [1024]
  *   G2V_OPT_GRID          SGNS-kernel workgroups, 0 = the staleness-bounded
  *                         default, RECOMPUTED by every g2v_set_vocab from the
- *                         vocabulary, and lowered for a Hogwild g2v_train call
- *                         whose hot syn0 rows would overshoot (the call's
- *                         largest alpha and |syn1neg|^2)
- *                         (g2v_get_option reads set_vocab's value; g2v_stats
- *                         reports the last launch's); > 0 = fixed, no cap [0]
+ *                         vocabulary; each Hogwild launch on it then trains
+ *                         only as many waves as keep the hot syn0 rows from
+ *                         overshooting (the launch's largest alpha and
+ *                         |syn1neg|^2 measured on the device just before it;
+ *                         DESIGN.md 5c; g2v_stats.sgns_waves); > 0 = fixed,
+ *                         every wave trains, no cap [0]
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
  *                         2 uncached (re-allocates, zero-filled) [0]
  *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
@@ -190,9 +194,9 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_DEBUG_FAIL_MERGE 18
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups g2v_set_vocab
- * chose -- by default the staleness budget's, at most one per CU; a Hogwild
- * g2v_train call may lower it further (the per-call stability cap), and
- * g2v_read_stats reports the grid and stripe layout the last launch used). */
+ * chose -- by default the staleness budget's, at most one per CU; the
+ * stability cap may hold some of their waves back in a launch, and
+ * g2v_read_stats reports the layout and the waves the last launch used). */
 int g2v_get_option(g2v_ctx *ctx, int key, int64_t *value);
 /* Row stride (floats) the device tables use. */
 int g2v_row_stride(g2v_ctx *ctx, int64_t *ld_out);

@@ -63,8 +63,10 @@ def main():
     ap.add_argument("--auc-seeds", default="0,1,2")
     ap.add_argument("--engines", default="gpu,oracle",
                     help="gpu (libg2v Hogwild), gpu_seq (libg2v sequential mode), gpu_gridN "
-                         "(Hogwild on N workgroups), oracle (sequential), oracle_hogN (the C "
-                         "restatement's OpenMP Hogwild on N threads: gensim workers=N)")
+                         "(Hogwild on N workgroups), gpu_uncapped (Hogwild fixed at set_vocab's "
+                         "default grid: no per-call stability cap), oracle (sequential), "
+                         "oracle_hogN (the C restatement's OpenMP Hogwild on N threads: gensim "
+                         "workers=N)")
     ap.add_argument("--per-iter", action="store_true", help="print the GPU runs' objective per iteration")
     ap.add_argument("--out", default="gpurun_out/e2e_parity")
     a = ap.parse_args()
@@ -105,7 +107,7 @@ def main():
     off = np.arange(0, 2 * n + 1, 2, dtype=np.int64)
     si, cum = CO.sample_int(vc, a.sample), CO.make_cum_table(vc)
     lockf = np.ones(V, np.float32)
-    log = {"config": {"pairs_total": n, "vocab": V, "modules": a.modules,
+    log = {"config": {"pairs_total": n, "vocab": V, "modules": a.modules, "p_tok_max": None,
                       "ggipnn_repeat": a.ggipnn_repeat, "iters": a.iters, "dim": D,
                       "negative": K, "sample": a.sample},
            "corpus_s": round(time.time() - t0, 1), "runs": {}}
@@ -114,8 +116,21 @@ def main():
     def tokens(it):
         return np.ascontiguousarray(tok0.reshape(n, 2)[perms[it]].reshape(-1))
 
+    # the stability cap's product (g2v_api.hip stability_grid): waves x p_tok_max
+    # x (K+1) x alpha x max |syn1neg[r]|^2, capped at 100
+    tot = float(vc.sum())
+    thr = a.sample * tot if 0 < a.sample < 1 else tot
+    pt = vc * np.minimum(1.0, (np.sqrt(vc / thr) + 1.0) * (thr / vc))
+    p_tok_max = float((pt / pt.sum()).max())
+    log["config"]["p_tok_max"] = p_tok_max
+
     def train_gpu(seed, mode=N.MODE_HOGWILD, grid=0, overlap=None):
         eng = E.SGNSEngine(V, D, K)
+        if grid == -1:  # set_vocab's default, fixed (no per-call cap)
+            probe = E.SGNSEngine(V, D, K)
+            probe.set_vocab(vc, a.sample)
+            grid = int(probe.get_option(N.OPT_GRID))
+            probe.close()
         if grid:
             eng.set_option(N.OPT_GRID, grid)
         if overlap is not None:
@@ -134,13 +149,16 @@ def main():
                 g0, g1 = eng.get_weights()
                 n0 = (g0.astype(np.float64) ** 2).sum(1)
                 n1 = (g1.astype(np.float64) ** 2).sum(1)
-                print(f"  gpu grid {grid} (call {eng.read_stats()['sgns_grid']}) seed {seed} "
+                cw = eng.read_stats()['sgns_waves']
+                prod = cw * p_tok_max * (K + 1) * float(al.max()) * n1.max()
+                print(f"  gpu grid {grid} (last launch {cw} waves, cap product at the call's "
+                      f"end {prod:.1f}) seed {seed} "
                       f"iteration {it + 1} heldin "
                       f"{RQ.heldin(g0, g1, tok0, vc, K, n=20000):.5f} |syn0|^2 max/top20 "
                       f"{n0.max():.2f}/{n0[:20].max():.2f} |syn1neg|^2 max/top20 "
                       f"{n1.max():.2f}/{n1[:20].max():.2f}", flush=True)
         st = eng.read_stats()
-        extra = {"grid": int(eng.get_option(N.OPT_GRID)), "last_call_grid": int(st["sgns_grid"])}
+        extra = {"grid": int(eng.get_option(N.OPT_GRID)), "last_launch_waves": int(st["sgns_waves"])}
         s0, s1 = eng.get_weights()
         eng.close()
         return s0, s1, {"loss": float(st["training_loss"]), **extra}
@@ -172,6 +190,8 @@ def main():
                 s0, s1, extra = train_gpu(seed, overlap=int(eng_name[6:]))
             elif eng_name.startswith("gpu_grid"):
                 s0, s1, extra = train_gpu(seed, grid=int(eng_name[8:]))
+            elif eng_name == "gpu_uncapped":
+                s0, s1, extra = train_gpu(seed, grid=-1)
             elif eng_name.startswith("oracle_hog"):
                 s0, s1, extra = train_oracle(seed, int(eng_name[10:]))
             else:

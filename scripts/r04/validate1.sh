@@ -1,9 +1,10 @@
 #!/bin/bash
-# round 4: first GPU pass over the new code (RCCL stand-in tests, dense e2e gate, stamps)
+# round 4: GPU pass over the new code: the whole -m gpu suite but the C3 gate,
+# then the stamped-kernel diagnostics (sample 0 and C2)
 set -o pipefail
 mkdir -p gpurun_out/r04v1
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_rccl_standin.py "tests/test_gpu_e2e_parity.py::test_gpu_end_to_end_dense_5k_genes" \
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread \
+  --deselect tests/test_gpu_c3_quality.py::test_c3_eight_replicas_within_one_percent_of_one_model \
   > gpurun_out/r04v1/tests.log 2>&1
 rc=$?
 echo "tests rc $rc" >> gpurun_out/r04v1/tests.log

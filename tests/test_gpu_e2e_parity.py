@@ -42,7 +42,7 @@ def _train_e2e(tmp_path, sample, grid=None, cfg=E2E):
     syn0 = E.seeded_vectors(wseeds, D)
     js = E.plan_jobs(n_sent=n, sent_len=2)
     al = E.job_alphas(js, n)
-    got = {"loss": [], "heldin": [], "target_ratio": [], "grid": [], "call_grid": []}
+    got = {"loss": [], "heldin": [], "target_ratio": [], "grid": [], "waves": []}
     for seed in cfg["seeds"]:
         eng = E.SGNSEngine(V, D, K)
         if grid:
@@ -60,7 +60,7 @@ def _train_e2e(tmp_path, sample, grid=None, cfg=E2E):
         eng.sync()
         st = eng.read_stats()
         got["grid"].append(int(eng.get_option(N.OPT_GRID)))
-        got["call_grid"].append(int(st["sgns_grid"]))
+        got["waves"].append(int(st["sgns_waves"]))  # the last launch's, after the cap
         s0, s1 = eng.get_weights()
         eng.close()
         kv = KeyedVectors(D)
@@ -103,16 +103,17 @@ def test_gpu_hogwild_sample0_stays_stable(tmp_path):
     """sample = 0 keeps the hottest genes' syn0 rows busy: past a staleness
     that grows with the vectors' norms a hot syn0 row overshoots at a
     sawtooth restart and freezes (|f| >= 6 skips every later update; DESIGN.md
-    5c).  g2v_train caps each call's grid for it (stability_grid): the
-    objective and the final loss track the sequential oracle's, and the cap
-    has engaged by the last call.  The target function is reported, not
+    5c).  k_sgns_atomic caps the waves that train in every launch for it (from
+    |syn1neg|^2 measured on the device just before the launch): the objective
+    and the final loss track the sequential oracle's, and the cap has engaged
+    by the last launch.  The target function is reported, not
     gated: at sample 0 the Hogwild staleness moves it a few percent on
     structured corpora."""
     ref = _golden()["sample0"]
     got = _train_e2e(tmp_path, 0.0)
     gaps = _gaps(got, ref)
     print("gpu sample 0", got, "gaps vs sequential oracle", gaps)
-    assert all(c < g for c, g in zip(got["call_grid"], got["grid"])), got
+    assert all(w < 4 * g for w, g in zip(got["waves"], got["grid"])), got
     assert abs(gaps["heldin"]) < 0.005, gaps
     assert abs(gaps["loss"]) < 0.01, gaps
 
