@@ -66,13 +66,15 @@ def test_device_shuffle_vocabulary_order(tmp_path):
 
 
 def test_device_shuffle_quality(tmp_path):
-    """the mean over two shuffle seeds of each mode's 3-iteration objective:
-    one run's own spread over seeds is ~0.6 % here (python 2.810-2.827,
-    device 2.808-2.820 over seeds 4-7, profiles/r03/r03f_spread.log), so a
-    single pair of runs cannot carry a sub-percent bar"""
+    """the mean over four shuffle seeds of each mode's 3-iteration objective
+    within 0.5 %: one run's own spread over seeds is ~0.6 % (python
+    2.810-2.827, device 2.808-2.820 over seeds 4-7, profiles/r03/r03f_spread.log:
+    sd ~0.25 %), so a single pair of runs cannot carry a sub-percent bar; the
+    difference of two 4-run means has an sd of ~0.18 %, and the 0.5 % bar sits
+    at ~2.8 of them (round 3 ran 2 seeds at 0.6 %)"""
     data, pairs, names = _corpus(tmp_path)
     loss = {"python": [], "device": []}
-    for seed in ("4", "5"):
+    for seed in ("4", "5", "6", "7"):
         base = ["--iters", "3", "--dim", "64", "--hash", "crc32", "--shuffle-seed", seed,
                 "--native-ingest", "--no-txt", "--no-w2v"]
         for mode in loss:
@@ -83,4 +85,4 @@ def test_device_shuffle_quality(tmp_path):
     la, lb = np.mean(loss["python"]), np.mean(loss["device"])
     print("held-in objective: python shuffle %s, device shuffle %s" % (loss["python"], loss["device"]))
     assert la < 0.9 * 6 * np.log(2)
-    assert abs(lb - la) <= 0.006 * la, (la, lb)
+    assert abs(lb - la) <= 0.005 * la, (la, lb)
