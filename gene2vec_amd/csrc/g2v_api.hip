@@ -669,7 +669,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
       return G2V_OK;
     case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 8, G2V_EINVAL, "debug write mode out of [0, 8]");
+      REQUIRE(value >= 0 && value <= 9, G2V_EINVAL, "debug write mode out of [0, 9]");
       c->debug_write = (int)value;
       return G2V_OK;
     case G2V_OPT_ATOMIC_OVERLAP:
@@ -1115,7 +1115,9 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   const int64_t max_rows2 = kStripeMaxBytes / (2 * 4 * (int64_t)(c->stripe2_copies - 1) * c->ld);
   const int r2 = (int)std::min<int64_t>(std::min(stripe2_rows_eff(c), c->V),
                                         (int64_t)s.stripe_rows + max_rows2);
-  const bool tier2 = striped && (c->debug_write == 0 || c->debug_write == 6 || c->debug_write == 8) &&
+  const bool tier2 = striped &&
+                     (c->debug_write == 0 || c->debug_write == 6 || c->debug_write == 8 ||
+                      c->debug_write == 9) &&
                      r2 > s.stripe_rows;
   s.stripe2_rows = tier2 ? r2 : s.stripe_rows;
   s.stripe2_copies = tier2 ? c->stripe2_copies : 1;

@@ -128,12 +128,14 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
 // record e of the chunk staged in LDS (k_sgns_atomic stages each chunk's
 // records once): tg / input / alpha as wave-uniform scalars; every main row is
 // requested before the first striped row's copies are waited on
-template <int K, int NV>
+__device__ __forceinline__ uint64_t stamp_time();
+template <int K, int NV, bool STAMP = false>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
                                              const int32_t* r, __amdgpu_buffer_rsrc_t r0,
                                              __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
                                              __amdgpu_buffer_rsrc_t rs2, int rowb,
-                                             const uint32_t (&loff)[NV]) {
+                                             const uint32_t (&loff)[NV],
+                                             uint64_t* t_main = nullptr) {
   x.tg[0] = __builtin_amdgcn_readfirstlane(r[0]);
   x.input = __builtin_amdgcn_readfirstlane(r[1]);
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
@@ -149,6 +151,7 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
       for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  if (STAMP) *t_main = stamp_time();  // main-row loads issued (diagnostic build)
   // ablation 6 (G2V_OPT_DEBUG_WRITE): copies are written but not read (the
   // throughput a drained-copy design would have; values go stale)
   const int R1 = a.skip_copy_reads ? 0 : a.stripe_rows;
@@ -172,7 +175,10 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // bytes, tables never written: a throughput probe), 4 the production f32
 // atomics into that scratch table (tables never written), 5 production atomics
 // on syn1neg only, syn0 never written (the ceiling of any syn0-side combining),
-// 8 production with s_memtime stamps per loop segment (diagnostic build)
+// 8 production with s_memtime stamps per loop segment (diagnostic build),
+// 9 production without each row's last atomic instruction (elements 192..255
+// at D <= 256: a throughput probe of the per-wave instruction count; breaks
+// training)
 //
 // One row's delta coef * src[0, D) as a FIXED 4 * NV wave-instructions: the
 // buffer resource spans the row's D floats, so lanes past D (and every lane of
@@ -193,9 +199,10 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
       reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), (short)0, nrec, 0x00020000);
 #pragma unroll
   for (int i = 0; i < 4 * NV; ++i) {
+    if (WR == 9 && i == 4 * NV - 1) continue;  // ablation: no tail instruction
     const int off = (64 * i + lane) * 4;
     const float v = coef * src[i];
-    if (WR == 0 || WR == 4 || WR == 5 || WR == 8)
+    if (WR == 0 || WR == 4 || WR == 5 || WR == 8 || WR == 9)
       __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
     else if (WR == 1)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
@@ -311,6 +318,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   // WR 8: cycle sums per segment (see g2v_debug_stamps), wave-uniform scalars
   constexpr int kAtomicsPerExample = 4 * NV * (NT + 1);  // emit_row's fixed count
   uint64_t acc[5] = {0, 0, 0, 0, 0};
+  uint64_t sub[4] = {0, 0, 0, 0};  // dots+reduce, LUT/gradients, first 4 rows' atomics, main loads
   uint64_t n_ex = 0, tl0 = 0, rl0 = 0;
   if (WR == 8) {
     rl0 = stamp_realtime();
@@ -361,6 +369,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         pd[d] = s;
       }
       wave_reduce_multi<NT>(pd, dot, lane);
+      uint64_t tsub = 0;
+      if (WR == 8) {
+        tsub = stamp_time();
+        sub[0] += tsub - ts;
+      }
       float4 work[NV];
 #pragma unroll
       for (int v = 0; v < NV; ++v) work[v] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -431,6 +444,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         dirty[d] = true;
         any = true;
       }
+      if (WR == 8) {
+        const uint64_t t = stamp_time();
+        sub[1] += t - tsub;
+      }
       // stage l1 / work in element order
 #pragma unroll
       for (int v = 0; v < NV; ++v) {
@@ -467,7 +484,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         acc[2] += t - ts;
         ts = t;
       }
-      if (e + 1 < e_end) load_example<K, NV>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff);
+      uint64_t tmain = ts;
+      if (e + 1 < e_end)
+        load_example<K, NV, WR == 8>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff, &tmain);
+      if (WR == 8) sub[3] += tmain - ts;
       if (WR == 8) {
         const uint64_t t = stamp_time();
         acc[3] += t - ts;
@@ -505,9 +525,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
       // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work
 #pragma unroll
-      for (int d = 0; d < NT; ++d)
+      for (int d = 0; d < NT; ++d) {
         emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb),
                          live[d], D, v1, g[d], lane);
+        if (WR == 8 && d == 3) sub[2] += stamp_time() - ts;  // 16 atomics issued
+      }
       emit_row<NV, WR>(upd_row<WR>(a, 0, input, cbase + NT, rowb),
                        any && WR != 5, D, vw, lf, lane);
       __builtin_amdgcn_wave_barrier();
@@ -527,6 +549,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       atomicAdd(o + 7, (unsigned long long)tl);
       atomicAdd(o + 8, (unsigned long long)rl);
       atomicAdd(o + 9, 1ull);
+      for (int i = 0; i < 4; ++i) atomicAdd(o + 10 + i, (unsigned long long)sub[i]);
     }
   }
 }
@@ -564,6 +587,10 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 8) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 9) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 9>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
 #endif

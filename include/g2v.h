@@ -134,7 +134,10 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         main-row-only reads, 8 = the production kernel with
  *                         s_memtime stamps per loop segment (diagnostic build,
  *                         K 5 / D <= 256: g2v_debug_stamps; its run time is
- *                         not a measurement, its segment SHARES are) [0]
+ *                         not a measurement, its segment SHARES are), 9 = the
+ *                         production kernel without each row's last atomic
+ *                         instruction (a probe of the per-wave instruction
+ *                         count; breaks training) [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE2_ROWS  second stripe tier: rows [STRIPE_ROWS, this) get
  *                         STRIPE2_COPIES copies each (<= STRIPE_ROWS = off);
@@ -290,7 +293,10 @@ int g2v_debug_sample(g2v_ctx *ctx, const int64_t *job_sent, const uint64_t *job_
  * (incl. summing striped rows' copies), [4] issuing this example's atomics,
  * [5] whole loop per wave (the rest is per-chunk work: record staging, the
  * work queue), [6] examples, [7] s_memtime ticks and [8] s_memrealtime ticks
- * (100 MHz) over the loops (clock = [7] / [8] x 100 MHz), [9] waves; n >= 10. */
+ * (100 MHz) over the loops (clock = [7] / [8] x 100 MHz), [9] waves; within
+ * [1]: [10] the dots and their cross-lane reduction, [11] the sigmoid lookups,
+ * gradients and row updates; within [4]: [12] the first 4 rows' atomics;
+ * within [3]: [13] the main-row loads; n >= 16. */
 int g2v_debug_stamps(g2v_ctx *ctx, uint64_t *out, int64_t n);
 
 /* ---- sync / stats ------------------------------------------------------------ */

@@ -37,6 +37,10 @@ def main():
     ap.add_argument("--sample", type=float, default=1e-3)
     ap.add_argument("--epochs", type=int, default=4)
     ap.add_argument("--grid", type=int, default=0)
+    ap.add_argument("--arms", default="production,stamped,production_again",
+                    help="production, stamped (debug write 8), notail (debug write 9: each "
+                         "row's last atomic instruction dropped, a throughput probe), copiesN "
+                         "(production with G2V_OPT_STRIPE_COPIES N), any suffix _again")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     D, K = 200, 5
@@ -62,8 +66,11 @@ def main():
     out = {"config": {"pairs": a.pairs, "vocab": a.vocab, "sample": a.sample, "D": D, "K": K},
            "arms": {}}
     buf = np.zeros(16, np.uint64)
-    for arm, dbg in (("production", 0), ("stamped", 8), ("production_again", 0)):
+    for arm in a.arms.split(","):
+        base = arm.replace("_again", "")
+        dbg = {"stamped": 8, "notail": 9}.get(base, 0)
         eng.set_option(N.OPT_DEBUG_WRITE, dbg)
+        eng.set_option(N.OPT_STRIPE_COPIES, int(base[6:]) if base.startswith("copies") else 0)
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)  # warm (and |syn1| grows)
         eng.read_stats()
         eng._lib.g2v_debug_stamps(eng._h, N.ptr(buf), 16)
@@ -73,7 +80,8 @@ def main():
         st = eng.read_stats()
         wall = time.time() - t
         N.check(eng._lib.g2v_debug_stamps(eng._h, N.ptr(buf), 16))
-        res = {"grid": st["sgns_grid"], "examples": st["examples"],
+        res = {"grid": st["sgns_grid"], "waves": st["sgns_waves"],
+               "stripes": f"{st['stripe_rows']}x{st['stripe_copies']}", "examples": st["examples"],
                "sgns_ms": round(st["sgns_kernel_ms"], 2), "wall_s": round(wall, 3),
                "examples_per_s": round(st["examples"] / (st["sgns_kernel_ms"] / 1e3), 1)}
         if dbg == 8:
@@ -82,6 +90,13 @@ def main():
             names_ = ["rows", "compute", "land", "prefetch", "atomics"]
             seg = {k: b[i] / n_ex for i, k in enumerate(names_)}
             seg["chunk"] = (b[5] - sum(b[:5])) / n_ex
+            seg["compute.dots_reduce"] = b[10] / n_ex
+            seg["compute.lut_grad_update"] = b[11] / n_ex
+            seg["compute.staging"] = (b[1] - b[10] - b[11]) / n_ex
+            seg["atomics.first16"] = b[12] / n_ex
+            seg["atomics.last12"] = (b[4] - b[12]) / n_ex
+            seg["prefetch.main_loads"] = b[13] / n_ex
+            seg["prefetch.stripe_copies"] = (b[3] - b[13]) / n_ex
             tot = b[5] / n_ex
             clock_mhz = b[7] / b[8] * 100.0
             res.update({"cycles_per_example_per_wave": round(tot, 1),
@@ -89,7 +104,7 @@ def main():
                         "segments_share": {k: round(v / tot, 4) for k, v in seg.items()},
                         "clock_MHz": round(clock_mhz, 1),
                         "period_us": round(tot / clock_mhz, 3),
-                        "waves": waves, "stamped_examples": n_ex})
+                        "wave_launches": waves, "stamped_examples": n_ex})
         out["arms"][arm] = res
         print(arm, json.dumps(res), flush=True)
     eng.close()
