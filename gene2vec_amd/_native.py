@@ -49,6 +49,7 @@ OPT_ACTIVE_WAVES = 15
 OPT_MERGE_BETA_MILLI = 16
 OPT_MERGE_GAMMA_MILLI = 17
 OPT_DEBUG_FAIL_MERGE = 18
+OPT_ATOMIC_TAILS = 19
 COLL_SUM = 0
 COLL_BCAST0 = 1
 BATCH_WORDS = 10000

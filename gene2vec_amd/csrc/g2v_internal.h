@@ -119,6 +119,7 @@ struct SgnsArgs {
   float cap_coef;           // p_tok_max x (K+1) x the launch's largest alpha
   float cap_budget;
   int* waves_out;           // the waves that trained (block 0 writes it)
+  int tail_combine;         // G2V_OPT_ATOMIC_TAILS (k_sgns_atomic TC)
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])

@@ -34,6 +34,10 @@ struct ExRegs {
   float alpha;
   float4 l1[NV];
   float4 rw[K + 1][NV];
+  // a striped hot row's copies, summed in copy order (cs[K + 1]: the syn0
+  // row); added to the main row once the main rows have landed (add_copies)
+  float4 cs[K + 2][NV];
+  bool cp[K + 2];
 };
 
 // row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
@@ -126,8 +130,15 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
 }
 
 // record e of the chunk staged in LDS (k_sgns_atomic stages each chunk's
-// records once): tg / input / alpha as wave-uniform scalars; every main row is
-// requested before the first striped row's copies are waited on
+// records once): tg / input / alpha as wave-uniform scalars.  The striped hot
+// rows' copies are requested FIRST and summed right away (nothing else is in
+// flight then: the previous example's atomics have landed), THEN every main
+// row is requested and left in flight: the caller issues its atomics behind
+// these loads and waits for them only at the next example's first use
+// (vmcnt(#atomics)).  Round 3 requested the main rows first and added the
+// copies into them here, and that wait on the main rows (the compiler waited
+// for all of them before the first copy sum) held every example's atomics
+// back by a full load latency (round 4 stamps).
 __device__ __forceinline__ uint64_t stamp_time();
 template <int K, int NV, bool STAMP = false>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
@@ -135,12 +146,30 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
                                              __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
                                              __amdgpu_buffer_rsrc_t rs2, int rowb,
                                              const uint32_t (&loff)[NV],
-                                             uint64_t* t_main = nullptr) {
+                                             uint64_t* t_copies = nullptr) {
   x.tg[0] = __builtin_amdgcn_readfirstlane(r[0]);
   x.input = __builtin_amdgcn_readfirstlane(r[1]);
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
 #pragma unroll
   for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
+  // ablation 6 (G2V_OPT_DEBUG_WRITE): copies are written but not read (the
+  // throughput a drained-copy design would have; values go stale)
+  const int R1 = a.skip_copy_reads ? 0 : a.stripe_rows;
+  const int R2 = a.skip_copy_reads ? 0 : a.stripe2_rows;
+#pragma unroll
+  for (int d = 0; d <= K + 1; ++d) {
+    const int t = d <= K ? x.tg[d] : x.input;
+    const int tbl = d <= K ? 1 : 0;
+    x.cp[d] = t >= 0 && t < R2;  // (R2 >= R1)
+    if (!x.cp[d]) continue;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x.cs[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (t < R1)
+      add_stripes<NV>(x.cs[d], rs, t, tbl, R1, a.stripe_copies, rowb, loff);
+    else
+      add_stripes<NV>(x.cs[d], rs2, t - R1, tbl, R2 - R1, a.stripe2_copies, rowb, loff);
+  }
+  if (STAMP) *t_copies = stamp_time();  // copies summed (diagnostic build)
   load_main<NV>(x.l1, r0, x.input, rowb, loff);
 #pragma unroll
   for (int d = 0; d <= K; ++d) {
@@ -151,22 +180,23 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
       for (int v = 0; v < NV; ++v) x.rw[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
-  if (STAMP) *t_main = stamp_time();  // main-row loads issued (diagnostic build)
-  // ablation 6 (G2V_OPT_DEBUG_WRITE): copies are written but not read (the
-  // throughput a drained-copy design would have; values go stale)
-  const int R1 = a.skip_copy_reads ? 0 : a.stripe_rows;
-  const int R2 = a.skip_copy_reads ? 0 : a.stripe2_rows;
-  if (x.input < R1)
-    add_stripes<NV>(x.l1, rs, x.input, 0, R1, a.stripe_copies, rowb, loff);
-  else if (x.input < R2)
-    add_stripes<NV>(x.l1, rs2, x.input - R1, 0, R2 - R1, a.stripe2_copies, rowb, loff);
+}
+
+// a striped row's value = main + (its copies summed in copy order), once the
+// main rows have landed
+template <int K, int NV>
+__device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
 #pragma unroll
-  for (int d = 0; d <= K; ++d) {
-    if (x.tg[d] < 0) continue;
-    if (x.tg[d] < R1)
-      add_stripes<NV>(x.rw[d], rs, x.tg[d], 1, R1, a.stripe_copies, rowb, loff);
-    else if (x.tg[d] < R2)
-      add_stripes<NV>(x.rw[d], rs2, x.tg[d] - R1, 1, R2 - R1, a.stripe2_copies, rowb, loff);
+  for (int d = 0; d <= K + 1; ++d) {
+    if (!x.cp[d]) continue;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      float4& o = d <= K ? x.rw[d][v] : x.l1[v];
+      o.x += x.cs[d][v].x;
+      o.y += x.cs[d][v].y;
+      o.z += x.cs[d][v].z;
+      o.w += x.cs[d][v].w;
+    }
   }
 }
 
@@ -187,7 +217,7 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // the compiler wait for the next example's row loads with vmcnt(#atomics)
 // instead of draining this example's atomics (vmcnt(0)) -- atomics retire in
 // the background while the wave computes.
-template <int NV, int WR>
+template <int NV, int WR, int NI = 4 * NV>
 __device__ __forceinline__ void emit_row(float* row, bool live, int D, const float (&src)[4 * NV],
                                          float coef, int lane) {
   // row and live are wave-uniform; say so, or the compiler waterfalls the resource
@@ -198,7 +228,7 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
       reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), (short)0, nrec, 0x00020000);
 #pragma unroll
-  for (int i = 0; i < 4 * NV; ++i) {
+  for (int i = 0; i < NI; ++i) {
     if (WR == 9 && i == 4 * NV - 1) continue;  // ablation: no tail instruction
     const int off = (64 * i + lane) * 4;
     const float v = coef * src[i];
@@ -254,8 +284,18 @@ __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
   return (int64_t)__builtin_amdgcn_readfirstlane(v);
 }
 
-template <int K, int NV, int WR = 0, bool LOSS = false>
+// TC (tail combine, NV = 1 and 192 < D <= 192 + 64 / (K + 2): the
+// reference's dim 200 with K 5): every row sends its first 192 elements as 3
+// full 256-B atomic instructions, and the K + 2 rows' short tails (D - 192
+// floats each) go out together in ONE instruction, lane l adding element
+// 192 + l % (D - 192) of row l / (D - 192): 3 (K + 2) + 1 instructions per
+// example instead of 4 (K + 2).  The memory side sees the same requests; the
+// wave issues 6 fewer vector-memory instructions at K 5, and a wave's atomics
+// stall on its outstanding vector-memory operations (round 4 stamps,
+// DESIGN.md 5d)
+template <int K, int NV, int WR = 0, bool LOSS = false, bool TC = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
+  static_assert(!TC || (NV == 1 && WR == 0), "tail combine: production kernel, D <= 256");
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
   constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
@@ -314,11 +354,19 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     loff[v] = (lane + 64 * v) < a.nvec ? (uint32_t)(lane * 16 + 1024 * v) : kLaneOob;
+  // TC: this lane's row (0..K: syn1neg targets, K+1: syn0) and element of the
+  // combined tail instruction; rows past K+1 send nothing
+  int tc_row = NT + 1, tc_el = 0;
+  if (TC) {
+    const int T = D - 192;
+    tc_row = lane / T;
+    tc_el = 192 + lane - tc_row * T;
+  }
 
   // WR 8: cycle sums per segment (see g2v_debug_stamps), wave-uniform scalars
   constexpr int kAtomicsPerExample = 4 * NV * (NT + 1);  // emit_row's fixed count
   uint64_t acc[5] = {0, 0, 0, 0, 0};
-  uint64_t sub[4] = {0, 0, 0, 0};  // dots+reduce, LUT/gradients, first 4 rows' atomics, main loads
+  uint64_t sub[4] = {0, 0, 0, 0};  // dots+reduce, LUT/gradients, first 4 rows' atomics, copies
   uint64_t n_ex = 0, tl0 = 0, rl0 = 0;
   if (WR == 8) {
     rl0 = stamp_realtime();
@@ -360,6 +408,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         ++n_ex;
       }
       // ---- compute example e ------------------------------------------------
+      add_copies<K, NV>(x);
       double pd[NT], dot[NT];
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
@@ -558,6 +607,31 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         continue;
       }
       // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work
+      if constexpr (TC) {
+        uint64_t tp = 0;  // this lane's tail destination, coefficient, liveness
+        float tcf = 0.f;
+        bool tok = false;
+#pragma unroll
+        for (int d = 0; d <= NT; ++d) {
+          float* row = d < NT ? upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb)
+                              : upd_row<WR>(a, 0, input, cbase + NT, rowb);
+          const bool lv = d < NT ? live[d] : any;
+          const float cf = d < NT ? g[d] : lf;
+          emit_row<NV, WR, 3>(row, lv, D, d < NT ? v1 : vw, cf, lane);
+          // lanes past row K+1 ride on the syn0 row's tail with a zero
+          if (tc_row == d || (d == NT && tc_row > NT)) {
+            tp = reinterpret_cast<uint64_t>(row);
+            tcf = cf;
+            tok = lv && tc_row <= NT;
+          }
+        }
+        const float tv = (tc_row < NT ? s1 : sw)[tc_el];
+        // unconditional (a skipped row's lanes add +0.0 to its tail): an
+        // exec-skip branch here would make the compiler wait for one of these
+        // atomics at the next example's first use of its rows
+        __builtin_amdgcn_global_atomic_fadd_f32(reinterpret_cast<float*>(tp) + tc_el,
+                                                tok ? tcf * tv : 0.0f);
+      } else {
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb),
@@ -566,6 +640,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
       emit_row<NV, WR>(upd_row<WR>(a, 0, input, cbase + NT, rowb),
                        any && WR != 5, D, vw, lf, lane);
+      }
       __builtin_amdgcn_wave_barrier();
       if (WR == 8) acc[4] += stamp_time() - ts;
       cbase = cbase + 1 == a.stripe_copies ? 0 : cbase + 1;
@@ -625,6 +700,18 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 9) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 9>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+#endif
+#if G2V_K == 5
+  // the reference's shape (dim 200, negative 5): combined row tails
+  if (nv == 1 && a.tail_combine && a.D > 192 && (a.D - 192) * (G2V_K + 2) <= 64) {
+    if (a.compute_loss)
+      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, true, true>), dim3(grid), dim3(kSgnsThreads), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, false, true>), dim3(grid), dim3(kSgnsThreads), 0,
+                         st, a);
     return hipGetLastError();
   }
 #endif

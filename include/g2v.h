@@ -172,6 +172,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         with G2V_OPT_GRID 1 and 1 wave the production kernel
  *                         runs its chunks in record order, a deterministic
  *                         update order (parity checks) [4]
+ *   G2V_OPT_ATOMIC_TAILS  Hogwild kernel at D 193..201 with negative 5 (the
+ *                         reference's dim 200): 1 = the K+2 rows' last D-192
+ *                         floats go out together in one atomic instruction
+ *                         (22 instead of 28 per example), 0 = one tail
+ *                         instruction per row [1]
  *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the
  *                         n-th in-call merge of every g2v_train call fails
  *                         before its collective, as a rank that dies between
@@ -195,6 +200,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_MERGE_BETA_MILLI 16
 #define G2V_OPT_MERGE_GAMMA_MILLI 17
 #define G2V_OPT_DEBUG_FAIL_MERGE 18
+#define G2V_OPT_ATOMIC_TAILS 19
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups g2v_set_vocab
  * chose -- by default the staleness budget's, at most one per CU; the
@@ -296,7 +302,8 @@ int g2v_debug_sample(g2v_ctx *ctx, const int64_t *job_sent, const uint64_t *job_
  * (100 MHz) over the loops (clock = [7] / [8] x 100 MHz), [9] waves; within
  * [1]: [10] the dots and their cross-lane reduction, [11] the sigmoid lookups,
  * gradients and row updates; within [4]: [12] the first 4 rows' atomics;
- * within [3]: [13] the main-row loads; n >= 16. */
+ * within [3]: [13] the striped rows' copies (requested and summed before the
+ * main rows are requested); n >= 16. */
 int g2v_debug_stamps(g2v_ctx *ctx, uint64_t *out, int64_t n);
 
 /* ---- sync / stats ------------------------------------------------------------ */

@@ -338,8 +338,8 @@ void orc_sgns_step_sequential(float *syn0, float *syn1neg, const float *lockf, i
  *     atomic): syn1neg[t] += g * l1 per applied target, then syn0[input] +=
  *     lockf * work;
  *   - hot-row stripes: rows [0, R1) of each table have C1-1 extra copies,
- *     rows [R1, R2) C2-1 (C2 a power of two); a read is main + copies summed in
- *     copy order; the delta of target d (d = K+1 for syn0) goes to copy
+ *     rows [R1, R2) C2-1 (C2 a power of two); a read is main + (the copies
+ *     summed in copy order from 0); the delta of target d (d = K+1 for syn0) goes to copy
  *     (cbase + d) mod C1 (tier 1) or (cbase + d) & (C2-1) (tier 2), copy 0 =
  *     the main row, cbase = e mod C1; after the launch every copy is folded
  *     into its main row in copy order and zeroed.
@@ -361,11 +361,16 @@ static float *orc_row(float *main, float *cp1, float *cp2, int64_t ld, int D, in
 
 static void orc_read_row(float *out, float *main, float *cp1, float *cp2, int64_t ld, int D,
                          int tbl, int32_t t, int R1, int C1, int R2, int C2) {
+    /* main + (copies summed in copy order from 0): the kernel sums a striped
+     * row's copies before its main row lands (load_example, round 4) */
     memcpy(out, main + (int64_t)t * ld, sizeof(float) * D);
     int C = t < R1 ? C1 : (t < R2 ? C2 : 1);
-    for (int c = 1; c < C; c++) {
-        const float *p = orc_row(main, cp1, cp2, ld, D, tbl, t, c, R1, C1, R2, C2);
-        for (int i = 0; i < D; i++) out[i] = out[i] + p[i];
+    if (C == 1) return;
+    for (int i = 0; i < D; i++) {
+        float cs = 0.0f;
+        for (int c = 1; c < C; c++)
+            cs = cs + orc_row(main, cp1, cp2, ld, D, tbl, t, c, R1, C1, R2, C2)[i];
+        out[i] = out[i] + cs;
     }
 }
 

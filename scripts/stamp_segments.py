@@ -40,7 +40,8 @@ def main():
     ap.add_argument("--arms", default="production,stamped,production_again",
                     help="production, stamped (debug write 8), notail (debug write 9: each "
                          "row's last atomic instruction dropped, a throughput probe), copiesN "
-                         "(production with G2V_OPT_STRIPE_COPIES N), any suffix _again")
+                         "(production with G2V_OPT_STRIPE_COPIES N), tailsN (production with "
+                         "G2V_OPT_ATOMIC_TAILS N), any suffix _again")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     D, K = 200, 5
@@ -71,6 +72,7 @@ def main():
         dbg = {"stamped": 8, "notail": 9}.get(base, 0)
         eng.set_option(N.OPT_DEBUG_WRITE, dbg)
         eng.set_option(N.OPT_STRIPE_COPIES, int(base[6:]) if base.startswith("copies") else 0)
+        eng.set_option(N.OPT_ATOMIC_TAILS, int(base[5:]) if base.startswith("tails") else 1)
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)  # warm (and |syn1| grows)
         eng.read_stats()
         eng._lib.g2v_debug_stamps(eng._h, N.ptr(buf), 16)
@@ -95,8 +97,8 @@ def main():
             seg["compute.staging"] = (b[1] - b[10] - b[11]) / n_ex
             seg["atomics.first16"] = b[12] / n_ex
             seg["atomics.last12"] = (b[4] - b[12]) / n_ex
-            seg["prefetch.main_loads"] = b[13] / n_ex
-            seg["prefetch.stripe_copies"] = (b[3] - b[13]) / n_ex
+            seg["prefetch.stripe_copies"] = b[13] / n_ex
+            seg["prefetch.main_loads"] = (b[3] - b[13]) / n_ex
             tot = b[5] / n_ex
             clock_mhz = b[7] / b[8] * 100.0
             res.update({"cycles_per_example_per_wave": round(tot, 1),
