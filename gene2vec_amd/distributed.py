@@ -320,6 +320,35 @@ class ThreadAgreement:
 
 MERGE_RULES = {"touch": 0, "mean": 1, "align": 2}  # == G2V_MERGE_TOUCH / _MEAN / _ALIGN
 
+# Data-parallel plan by shard size (8 replicas vs one
+# model through the reference's 10-iteration flow, C3's corpus shape): at
+# >= 125 M pairs per rank the touch rule every 4,096 jobs holds the SGNS
+# objective, the target function and GGIPNN AUC within 1 % (C3: held-in
+# -0.002 %, held-out -0.06 %, target +0.4 %; tests/test_gpu_c3_quality.py);
+# from 50 M pairs per rank the align rule at 7 merges per epoch does (three
+# runs: held-in +0.15..+0.41 %, held-out -0.06..-0.21 %, target -0.18..+0.24 %,
+# AUC +0.16..+0.33 %), where the touch rule reads -3.6 % on the target
+# function; below 50 M no measured rule or cadence holds the target function
+# (12.5 M: -2.6 % at best), so the CLI trains the corpus whole on every rank.
+DP_TOUCH_MIN_PAIRS = 125_000_000
+DP_MIN_PAIRS = 50_000_000
+DP_ALIGN_MERGES_PER_EPOCH = 7
+
+
+def dp_merge_plan(pairs_per_rank, merge_every_jobs=4096, rule="auto", jobs_per_rank=None):
+    """(rule, merge_every_jobs) for a data-parallel run: rule "auto" picks
+    touch at merge_every_jobs from DP_TOUCH_MIN_PAIRS pairs per rank, else
+    align with DP_ALIGN_MERGES_PER_EPOCH merges per epoch (jobs_per_rank:
+    gensim jobs of one rank's epoch; by default a pairs corpus's, 5,000 pairs
+    per 10,000-word job); an explicit rule keeps merge_every_jobs"""
+    if rule != "auto":
+        return rule, int(merge_every_jobs)
+    if pairs_per_rank >= DP_TOUCH_MIN_PAIRS:
+        return "touch", int(merge_every_jobs)
+    if jobs_per_rank is None:
+        jobs_per_rank = -(-int(pairs_per_rank) // 5000)
+    return "align", max(1, -(-int(jobs_per_rank) // DP_ALIGN_MERGES_PER_EPOCH))
+
 
 class ReplicaTrainer:
     """Drives one rank: trains job windows on an engine-like object and

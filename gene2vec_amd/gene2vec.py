@@ -237,18 +237,25 @@ def main(argv=None):
                              "written, as src/gene2vec.py:86 does (the kept in-memory model "
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
     parser.add_argument("--merge-every-jobs", type=int, default=4096,
-                        help="data-parallel replica merge cadence (gensim jobs per rank; "
-                             "4096 = 7 merges per epoch at C3, DESIGN.md section 7a)")
+                        help="data-parallel replica merge cadence of the touch rule (gensim "
+                             "jobs per rank; 4096 = 7 merges per epoch at C3, DESIGN.md 7a)")
+    parser.add_argument("--merge-rule", choices=("auto", "touch", "align", "mean"),
+                        default="auto",
+                        help="data-parallel replica merge rule: auto = touch every "
+                             "--merge-every-jobs jobs from 125 M pairs per rank, align at 7 "
+                             "merges per epoch from 50 M (the settings measured within 1 %% of "
+                             "one model, DESIGN.md 7a/7b); an explicit rule uses "
+                             "--merge-every-jobs")
     parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
                         default="auto",
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
                              "collective (gloo) = auto; torch = torch-owned tables merged by "
                              "torch.distributed")
-    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=125_000_000,
+    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=50_000_000,
                         help="under torchrun, shard the pairs only when every rank gets at least "
                              "this many; a smaller corpus trains whole on every rank (no merges, "
-                             "rank 0 writes): merged replicas of small shards learn far less "
-                             "than one model (DESIGN.md 7b)")
+                             "rank 0 writes): merged replicas of smaller shards lag one model on "
+                             "the target function whatever the rule (DESIGN.md 7b)")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "
@@ -363,7 +370,12 @@ def main(argv=None):
                   sg=1, negative=args.negative, sample=args.sample, hashfxn=hashfxn,
                   device=args.device, mode=args.mode, data_parallel=shard, grid=args.grid)
         import gene2vec_amd.word2vec as W
-        W.DP_MERGE_EVERY_JOBS = args.merge_every_jobs
+        from . import distributed as Dd
+        W.DP_MERGE_RULE, W.DP_MERGE_EVERY_JOBS = Dd.dp_merge_plan(
+            n_pairs / max(1, dworld), args.merge_every_jobs, args.merge_rule)
+        if shard:
+            print(f"data parallel: {dworld} ranks x {n_pairs // dworld} pairs, {W.DP_MERGE_RULE} "
+                  f"merge every {W.DP_MERGE_EVERY_JOBS} jobs")
         W.DP_MERGE_TRANSPORT = args.merge_transport
         model = None
         for current_iter in range(1, args.iters + 1):

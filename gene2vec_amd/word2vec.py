@@ -301,6 +301,9 @@ DP_MERGE_EVERY_JOBS = 4096
 # libg2v over the host collective for gloo; "torch" = torch-owned tables merged
 # by torch.distributed (the CLI's --merge-transport)
 DP_MERGE_TRANSPORT = "auto"
+# merge rule of data-parallel training (the CLI picks it by shard size:
+# distributed.dp_merge_plan)
+DP_MERGE_RULE = "touch"
 
 
 def crc32_hash(s):
@@ -380,6 +383,7 @@ class Word2Vec:
         self.data_parallel = data_parallel
         self.grid = int(grid)
         self.merge_every_jobs = DP_MERGE_EVERY_JOBS
+        self.merge_rule = DP_MERGE_RULE
         self.random = np.random.RandomState(seed)
         self.corpus_count = 0
         self.corpus_total_words = 0
@@ -482,12 +486,12 @@ class Word2Vec:
             dist.broadcast_object_list(box, src=0)
             eng.comm_init(box[0], world, rank)
             self._replica = Dd.ReplicaTrainer(eng, (), self.merge_every_jobs, mode,
-                                              backend="libg2v")
+                                              merge=self.merge_rule, backend="libg2v")
             return
         if transport == "host":
             eng.comm_init_host(Dd.host_collective(), world, rank)
             self._replica = Dd.ReplicaTrainer(eng, (), self.merge_every_jobs, mode,
-                                              backend="libg2v")
+                                              merge=self.merge_rule, backend="libg2v")
             return
         if transport != "torch":
             raise ValueError(f"merge transport {transport!r}")
@@ -503,7 +507,7 @@ class Word2Vec:
         dist.broadcast(tables, src=0)
         eng.bind_tables(tables[0].data_ptr(), tables[1].data_ptr(), eng.ld, keepalive=(tables,))
         self._replica = Dd.ReplicaTrainer(eng, (tables,), self.merge_every_jobs, mode,
-                                          backend="torch")
+                                          merge=self.merge_rule, backend="torch")
 
     def _ensure_engine(self):
         if self._engine is not None:
@@ -734,6 +738,7 @@ class Word2Vec:
         m.data_parallel = False
         m.grid = 0
         m.merge_every_jobs = DP_MERGE_EVERY_JOBS
+        m.merge_rule = DP_MERGE_RULE
         m.total_train_time = 0.0
         m.running_training_loss = float(meta.get("running_training_loss", 0.0))
         m.random = np.random.RandomState()

@@ -23,7 +23,8 @@ def test_cli_defaults_match_the_c3_gate():
     jobs and sharding from 125 M pairs per rank; the reference's own settings
     (src/gene2vec.py:57-63) stay the CLI's"""
     a = _parsed(["d", "o", "txt"])
-    assert a["merge_every_jobs"] == 4096 and a["dp_min_pairs_per_rank"] == 125_000_000
+    assert a["merge_every_jobs"] == 4096 and a["dp_min_pairs_per_rank"] == 50_000_000
+    assert a["merge_rule"] == "auto"
     assert (a["dim"], a["negative"], a["window"], a["sample"], a["iters"], a["workers"]) == \
         (200, 5, 1, 1e-3, 10, 32)
     assert a["grid"] == 0
@@ -37,3 +38,19 @@ def test_sample0_warns_about_the_target_function(capsys):
     assert "--sample 0" not in capsys.readouterr().err
     _parsed(["d", "o", "txt"])
     assert "warning" not in capsys.readouterr().err
+
+
+def test_dp_merge_plan_by_shard_size():
+    """distributed.dp_merge_plan: touch every 4,096 jobs from 125 M pairs per
+    rank (C3, tests/test_gpu_c3_quality.py), align at 7 merges per epoch from
+    50 M (tests/test_gpu_c3_quality.py's 50 M gate); explicit rules keep the
+    cadence"""
+    from gene2vec_amd import distributed as Dd
+    assert Dd.dp_merge_plan(125_000_000) == ("touch", 4096)
+    assert Dd.dp_merge_plan(1_000_000_000, 1024) == ("touch", 1024)
+    # 50 M pairs = 10,000 jobs of 5,000 pairs -> every 1,429 jobs = 7 merges
+    assert Dd.dp_merge_plan(50_000_000) == ("align", 1429)
+    rule, every = Dd.dp_merge_plan(80_000_000)
+    assert rule == "align" and -(-16_000 // every) == 7
+    assert Dd.dp_merge_plan(50_000_000, 4096, "touch") == ("touch", 4096)
+    assert Dd.dp_merge_plan(60_000_000, 333, "mean") == ("mean", 333)
