@@ -19,8 +19,7 @@ timeout -k 10 300 python -u scripts/stamp_segments.py --sample 1e-3 --pairs 2000
   --out gpurun_out/r04c4/stamps_c2.json > gpurun_out/r04c4/stamps_c2.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > gpurun_out/r04c4/bench.json 2> gpurun_out/r04c4/bench.err &&
 timeout -k 10 200 python -u bench.py --sample 0 --no-cpu-baseline > gpurun_out/r04c4/bench_s0.json 2> gpurun_out/r04c4/bench_s0.err &&
-timeout -k 10 300 python -u bench.py --vocab 60000 --dim 512 --negative 15 --no-cpu-baseline > gpurun_out/r04c4/bench_c4.json 2> gpurun_out/r04c4/bench_c4.err
-&&
+timeout -k 10 300 python -u bench.py --vocab 60000 --dim 512 --negative 15 --no-cpu-baseline > gpurun_out/r04c4/bench_c4.json 2> gpurun_out/r04c4/bench_c4.err &&
 timeout -k 10 400 python -u scripts/replica_quality.py --replicas 8 --pairs-per-replica 80000000 \
   --iters 10 --ggipnn-repeat 3 --modules 1000 --p-module 0.5 --merge-every 2288 --rules align \
   --auc-seeds 0 --out gpurun_out/rq_80m_align > gpurun_out/r04_rq_80m_align.log 2>&1
