@@ -345,6 +345,9 @@ def main():
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
                 "traffic_source": traffic_src,
                 "kernel_src_sha16": ksha,
+                # waves that trained in the last timed launch (the stability
+                # cap may hold some back)
+                "waves_last_launch": st["sgns_waves"],
                 **launch}
 
     # ---- measured gather roof: the same kernel on the same index
