@@ -50,6 +50,7 @@ OPT_MERGE_BETA_MILLI = 16
 OPT_MERGE_GAMMA_MILLI = 17
 OPT_DEBUG_FAIL_MERGE = 18
 OPT_ATOMIC_TAILS = 19
+OPT_COPY_DEFER = 20
 COLL_SUM = 0
 COLL_BCAST0 = 1
 BATCH_WORDS = 10000

@@ -148,6 +148,7 @@ struct g2v_ctx {
   int64_t stripe2_cap = 0;
   int atomic_overlap = 1;
   int atomic_tails = 1;  // G2V_OPT_ATOMIC_TAILS
+  int copy_defer = 1;    // G2V_OPT_COPY_DEFER
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int64_t debug_fail_merge = 0;  // G2V_OPT_DEBUG_FAIL_MERGE: fault injection
@@ -708,6 +709,10 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value == 0 || value == 1, G2V_EINVAL, "atomic tails must be 0 or 1");
       c->atomic_tails = (int)value;
       return G2V_OK;
+    case G2V_OPT_COPY_DEFER:
+      REQUIRE(value == 0 || value == 1, G2V_EINVAL, "copy defer must be 0 or 1");
+      c->copy_defer = (int)value;
+      return G2V_OK;
     case G2V_OPT_DEBUG_FAIL_MERGE:
       REQUIRE(value >= 0, G2V_EINVAL, "debug fail merge < 0");
       c->debug_fail_merge = value;
@@ -743,6 +748,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_MERGE_GAMMA_MILLI: *out = (int64_t)lrintf(c->merge_gamma * 1000.0f); return G2V_OK;
     case G2V_OPT_DEBUG_FAIL_MERGE: *out = c->debug_fail_merge; return G2V_OK;
     case G2V_OPT_ATOMIC_TAILS: *out = c->atomic_tails; return G2V_OK;
+    case G2V_OPT_COPY_DEFER: *out = c->copy_defer; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -1107,6 +1113,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.stripe_copies = striped ? copies : 1;
   s.overlap = c->atomic_overlap;
   s.tail_combine = c->debug_write == 0 ? c->atomic_tails : 0;
+  s.copy_defer = (c->debug_write == 0 || c->debug_write == 8) ? c->copy_defer : 0;
   s.active_waves = c->active_waves;
   s.queue = c->d_queue;
   int rc;

@@ -120,6 +120,7 @@ struct SgnsArgs {
   float cap_budget;
   int* waves_out;           // the waves that trained (block 0 writes it)
   int tail_combine;         // G2V_OPT_ATOMIC_TAILS (k_sgns_atomic TC)
+  int copy_defer;           // G2V_OPT_COPY_DEFER (k_sgns_atomic DC)
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])

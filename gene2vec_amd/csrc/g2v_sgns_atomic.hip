@@ -27,6 +27,9 @@ namespace g2v {
 // behind e+1's compute.  l1 and work are staged through LDS in element order
 // so each atomic wave-instruction adds 64 contiguous floats (256 B); the
 // row's buffer resource drops the lanes past D.
+constexpr int kStripeBatch = 7;
+constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
+
 template <int K, int NV>
 struct ExRegs {
   int32_t tg[K + 1];
@@ -38,6 +41,9 @@ struct ExRegs {
   // row); added to the main row once the main rows have landed (add_copies)
   float4 cs[K + 2][NV];
   bool cp[K + 2];
+  // DC: a striped row's last (up to kStripeBatch) copies, left in flight with
+  // the main rows and added to cs in copy order at add_copies
+  float4 dc[K + 2][kStripeBatch][NV];
 };
 
 // row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
@@ -59,21 +65,21 @@ __device__ __forceinline__ void load_main(float4 (&o)[NV], __amdgpu_buffer_rsrc_
 // The copies are loaded kStripeBatch at a time and summed in copy order, so a
 // striped row costs one memory latency per batch, not one per copy; copies
 // past stripe_copies read an out-of-range offset (zeros, no memory access).
-constexpr int kStripeBatch = 7;
-constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
 // t: the row's index within its tier, rows / C: the tier's row count and copies
 template <int NV>
 __device__ __forceinline__ void add_stripes(float4 (&o)[NV], __amdgpu_buffer_rsrc_t rs, int t,
                                             int tbl, int rows, int C, int rowb,
-                                            const uint32_t (&loff)[NV]) {
-  for (int c0 = 1; c0 < C; c0 += kStripeBatch) {
+                                            const uint32_t (&loff)[NV], int c_end = -1) {
+  // copies [1, c_end) (default: all C - 1 of them)
+  if (c_end < 0) c_end = C;
+  for (int c0 = 1; c0 < c_end; c0 += kStripeBatch) {
     float4 q[kStripeBatch][NV];
 #pragma unroll
     for (int j = 0; j < kStripeBatch; ++j) {
       const int c = c0 + j;
       const uint32_t base =
-          c < C ? (uint32_t)((int)stripe_row(tbl, t, c, rows, C) * rowb)
-                : (uint32_t)kStripeOob;
+          c < c_end ? (uint32_t)((int)stripe_row(tbl, t, c, rows, C) * rowb)
+                    : (uint32_t)kStripeOob;
 #pragma unroll
       for (int v = 0; v < NV; ++v) q[j][v] = bload4<0>(rs, (int)(base + loff[v]));
     }
@@ -140,7 +146,13 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
 // for all of them before the first copy sum) held every example's atomics
 // back by a full load latency (round 4 stamps).
 __device__ __forceinline__ uint64_t stamp_time();
-template <int K, int NV, bool STAMP = false>
+//
+// DC (NV = 1): a striped row's last min(C - 1, kStripeBatch) copies are not
+// waited for either: they are requested after every row's earlier copies have
+// been summed and before the main rows, and stay in flight with them (at
+// sample 0's 8 copies per row: all of them, so the prefetch waits for
+// nothing); add_copies adds them to cs in copy order, so the value is the same.
+template <int K, int NV, bool STAMP = false, bool DC = false>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
                                              const int32_t* r, __amdgpu_buffer_rsrc_t r0,
                                              __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
@@ -164,10 +176,33 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
     if (!x.cp[d]) continue;
 #pragma unroll
     for (int v = 0; v < NV; ++v) x.cs[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int C = t < R1 ? a.stripe_copies : a.stripe2_copies;
+    const int c_end = DC ? (C - 1 > kStripeBatch ? C - kStripeBatch : 1) : C;  // summed now
     if (t < R1)
-      add_stripes<NV>(x.cs[d], rs, t, tbl, R1, a.stripe_copies, rowb, loff);
+      add_stripes<NV>(x.cs[d], rs, t, tbl, R1, C, rowb, loff, c_end);
     else
-      add_stripes<NV>(x.cs[d], rs2, t - R1, tbl, R2 - R1, a.stripe2_copies, rowb, loff);
+      add_stripes<NV>(x.cs[d], rs2, t - R1, tbl, R2 - R1, C, rowb, loff, c_end);
+  }
+  if constexpr (DC) {
+#pragma unroll
+    for (int d = 0; d <= K + 1; ++d) {
+      if (!x.cp[d]) continue;
+      const int t = d <= K ? x.tg[d] : x.input;
+      const int tbl = d <= K ? 1 : 0;
+      const bool t1 = t < R1;
+      const int C = t1 ? a.stripe_copies : a.stripe2_copies;
+      const int rows = t1 ? R1 : R2 - R1;
+      const int tt = t1 ? t : t - R1;
+      const int c_beg = C - 1 > kStripeBatch ? C - kStripeBatch : 1;
+#pragma unroll
+      for (int j = 0; j < kStripeBatch; ++j) {
+        const int c = c_beg + j;
+        const uint32_t base =
+            c < C ? (uint32_t)((int)stripe_row(tbl, tt, c, rows, C) * rowb) : (uint32_t)kStripeOob;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) x.dc[d][j][v] = bload4<0>(t1 ? rs : rs2, (int)(base + loff[v]));
+      }
+    }
   }
   if (STAMP) *t_copies = stamp_time();  // copies summed (diagnostic build)
   load_main<NV>(x.l1, r0, x.input, rowb, loff);
@@ -184,11 +219,22 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 
 // a striped row's value = main + (its copies summed in copy order), once the
 // main rows have landed
-template <int K, int NV>
+template <int K, int NV, bool DC = false>
 __device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
 #pragma unroll
   for (int d = 0; d <= K + 1; ++d) {
     if (!x.cp[d]) continue;
+    if constexpr (DC) {
+#pragma unroll
+      for (int j = 0; j < kStripeBatch; ++j)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+          x.cs[d][v].x += x.dc[d][j][v].x;
+          x.cs[d][v].y += x.dc[d][j][v].y;
+          x.cs[d][v].z += x.dc[d][j][v].z;
+          x.cs[d][v].w += x.dc[d][j][v].w;
+        }
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       float4& o = d <= K ? x.rw[d][v] : x.l1[v];
@@ -293,9 +339,10 @@ __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
 // wave issues 6 fewer vector-memory instructions at K 5, and a wave's atomics
 // stall on its outstanding vector-memory operations (round 4 stamps,
 // DESIGN.md 5d)
-template <int K, int NV, int WR = 0, bool LOSS = false, bool TC = false>
+template <int K, int NV, int WR = 0, bool LOSS = false, bool TC = false, bool DC = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   static_assert(!TC || (NV == 1 && WR == 0), "tail combine: production kernel, D <= 256");
+  static_assert(!DC || NV == 1, "deferred copies: D <= 256");
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
   constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
@@ -390,7 +437,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
     int cbase = (int)(e_beg % (int64_t)a.stripe_copies);
     float lsum = 0.f;
     ExRegs<K, NV> x;
-    load_example<K, NV>(x, a, sr, r0, r1, rs, rs2, rowb, loff);
+    load_example<K, NV, false, DC>(x, a, sr, r0, r1, rs, rs2, rowb, loff);
     // drain here, so the loop head only waits on the back edge's count
     // (vmcnt(#atomics of the previous example)); without it the two incoming
     // paths merge to vmcnt(0), which also waits for the previous atomics
@@ -408,7 +455,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         ++n_ex;
       }
       // ---- compute example e ------------------------------------------------
-      add_copies<K, NV>(x);
+      add_copies<K, NV, DC>(x);
       double pd[NT], dot[NT];
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
@@ -569,7 +616,8 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
       uint64_t tmain = ts;
       if (e + 1 < e_end)
-        load_example<K, NV, WR == 8>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff, &tmain);
+        load_example<K, NV, WR == 8, DC>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff,
+                                         &tmain);
       if (WR == 8) sub[3] += tmain - ts;
       if (WR == 8) {
         const uint64_t t = stamp_time();
@@ -695,7 +743,11 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
     return hipGetLastError();
   }
   if (nv == 1 && a.debug_write == 8) {
-    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    if (a.copy_defer)
+      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8, false, false, true>), dim3(grid),
+                         dim3(kSgnsThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
   if (nv == 1 && a.debug_write == 9) {
@@ -706,15 +758,33 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
 #if G2V_K == 5
   // the reference's shape (dim 200, negative 5): combined row tails
   if (nv == 1 && a.tail_combine && a.D > 192 && (a.D - 192) * (G2V_K + 2) <= 64) {
-    if (a.compute_loss)
-      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, true, true>), dim3(grid), dim3(kSgnsThreads), 0,
-                         st, a);
-    else
-      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, false, true>), dim3(grid), dim3(kSgnsThreads), 0,
-                         st, a);
+    if (a.copy_defer) {
+      if (a.compute_loss)
+        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, true, true, true>), dim3(grid),
+                           dim3(kSgnsThreads), 0, st, a);
+      else
+        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, false, true, true>), dim3(grid),
+                           dim3(kSgnsThreads), 0, st, a);
+    } else {
+      if (a.compute_loss)
+        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, true, true>), dim3(grid), dim3(kSgnsThreads),
+                           0, st, a);
+      else
+        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, false, true>), dim3(grid), dim3(kSgnsThreads),
+                           0, st, a);
+    }
     return hipGetLastError();
   }
 #endif
+  if (nv == 1 && a.copy_defer) {
+    if (a.compute_loss)
+      hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true, false, true>), dim3(grid),
+                         dim3(kSgnsThreads), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, false, false, true>), dim3(grid),
+                         dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
   if (a.compute_loss) {
     if (nv == 1)
       hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true>), dim3(grid), dim3(kSgnsThreads), 0, st,

@@ -177,6 +177,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         floats go out together in one atomic instruction
  *                         (22 instead of 28 per example), 0 = one tail
  *                         instruction per row [1]
+ *   G2V_OPT_COPY_DEFER    Hogwild kernel at D <= 256: 1 = a striped row's last
+ *                         (up to 7) copies stay in flight with the main rows
+ *                         under the previous example's atomics and are summed
+ *                         at first use, 0 = every copy is summed before the
+ *                         main rows are requested (same values either way) [1]
  *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the
  *                         n-th in-call merge of every g2v_train call fails
  *                         before its collective, as a rank that dies between
@@ -201,6 +206,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_MERGE_GAMMA_MILLI 17
 #define G2V_OPT_DEBUG_FAIL_MERGE 18
 #define G2V_OPT_ATOMIC_TAILS 19
+#define G2V_OPT_COPY_DEFER 20
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups g2v_set_vocab
  * chose -- by default the staleness budget's, at most one per CU; the

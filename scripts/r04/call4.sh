@@ -12,10 +12,10 @@ rc=$?
 echo "tests rc $rc" >> gpurun_out/r04c4/tests.log
 [ $rc -le 1 ] || exit $rc
 timeout -k 10 300 python -u scripts/stamp_segments.py --sample 0 --grid 162 --pairs 20000000 \
-  --arms production,stamped,tails0,production_again,tails0_again \
+  --arms production,stamped,stamped_defer0,tails0,defer0,production_again,tails0_again,defer0_again \
   --out gpurun_out/r04c4/stamps_s0.json > gpurun_out/r04c4/stamps_s0.log 2>&1 &&
 timeout -k 10 300 python -u scripts/stamp_segments.py --sample 1e-3 --pairs 20000000 \
-  --arms production,stamped,tails0,production_again,tails0_again \
+  --arms production,stamped,stamped_defer0,tails0,defer0,production_again,tails0_again,defer0_again \
   --out gpurun_out/r04c4/stamps_c2.json > gpurun_out/r04c4/stamps_c2.log 2>&1 &&
 timeout -k 10 300 python -u bench.py > gpurun_out/r04c4/bench.json 2> gpurun_out/r04c4/bench.err &&
 timeout -k 10 200 python -u bench.py --sample 0 --no-cpu-baseline > gpurun_out/r04c4/bench_s0.json 2> gpurun_out/r04c4/bench_s0.err &&

@@ -41,7 +41,8 @@ def main():
                     help="production, stamped (debug write 8), notail (debug write 9: each "
                          "row's last atomic instruction dropped, a throughput probe), copiesN "
                          "(production with G2V_OPT_STRIPE_COPIES N), tailsN (production with "
-                         "G2V_OPT_ATOMIC_TAILS N), any suffix _again")
+                         "G2V_OPT_ATOMIC_TAILS N), deferN (production with G2V_OPT_COPY_DEFER "
+                         "N), stamped_deferN, any suffix _again")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     D, K = 200, 5
@@ -69,10 +70,11 @@ def main():
     buf = np.zeros(16, np.uint64)
     for arm in a.arms.split(","):
         base = arm.replace("_again", "")
-        dbg = {"stamped": 8, "notail": 9}.get(base, 0)
+        dbg = 8 if base.startswith("stamped") else {"notail": 9}.get(base, 0)
         eng.set_option(N.OPT_DEBUG_WRITE, dbg)
         eng.set_option(N.OPT_STRIPE_COPIES, int(base[6:]) if base.startswith("copies") else 0)
         eng.set_option(N.OPT_ATOMIC_TAILS, int(base[5:]) if base.startswith("tails") else 1)
+        eng.set_option(N.OPT_COPY_DEFER, int(base[-1]) if "defer" in base else 1)
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)  # warm (and |syn1| grows)
         eng.read_stats()
         eng._lib.g2v_debug_stamps(eng._h, N.ptr(buf), 16)
