@@ -293,7 +293,10 @@ def main():
     launch = {"grid_workgroups": st["sgns_grid"],
               "stripes": f"{st['stripe_rows']}x{st['stripe_copies']}",
               "stripes_tier2": (f"rows < {st['stripe2_rows']} x{st['stripe2_copies']}"
-                                if st["stripe2_copies"] > 1 else "off")}
+                                if st["stripe2_copies"] > 1 else "off"),
+              # kernel variants chosen at launch (same sources, other instances)
+              "atomic_tails": eng.get_option(N.OPT_ATOMIC_TAILS),
+              "copy_defer": eng.get_option(N.OPT_COPY_DEFER)}
     cands = [a.traffic_json] if a.traffic_json else sorted(
         glob.glob(os.path.join(ROOT, "profiles", "**", "traffic_r*.json"), recursive=True),
         reverse=True)

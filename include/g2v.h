@@ -176,7 +176,8 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         reference's dim 200): 1 = the K+2 rows' last D-192
  *                         floats go out together in one atomic instruction
  *                         (22 instead of 28 per example), 0 = one tail
- *                         instruction per row [1]
+ *                         instruction per row [0: one instruction over seven
+ *                         rows measured 1.5-4 % slower, DESIGN.md 5d]
  *   G2V_OPT_COPY_DEFER    Hogwild kernel at D <= 256: 1 = a striped row's last
  *                         (up to 7) copies stay in flight with the main rows
  *                         under the previous example's atomics and are summed

@@ -68,13 +68,15 @@ def main():
     out = {"config": {"pairs": a.pairs, "vocab": a.vocab, "sample": a.sample, "D": D, "K": K},
            "arms": {}}
     buf = np.zeros(16, np.uint64)
+    tails0 = eng.get_option(N.OPT_ATOMIC_TAILS)  # the library's defaults = "production"
+    defer0 = eng.get_option(N.OPT_COPY_DEFER)
     for arm in a.arms.split(","):
         base = arm.replace("_again", "")
         dbg = 8 if base.startswith("stamped") else {"notail": 9}.get(base, 0)
         eng.set_option(N.OPT_DEBUG_WRITE, dbg)
         eng.set_option(N.OPT_STRIPE_COPIES, int(base[6:]) if base.startswith("copies") else 0)
-        eng.set_option(N.OPT_ATOMIC_TAILS, int(base[5:]) if base.startswith("tails") else 1)
-        eng.set_option(N.OPT_COPY_DEFER, int(base[-1]) if "defer" in base else 1)
+        eng.set_option(N.OPT_ATOMIC_TAILS, int(base[5:]) if base.startswith("tails") else tails0)
+        eng.set_option(N.OPT_COPY_DEFER, int(base[-1]) if "defer" in base else defer0)
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)  # warm (and |syn1| grows)
         eng.read_stats()
         eng._lib.g2v_debug_stamps(eng._h, N.ptr(buf), 16)
