@@ -104,3 +104,39 @@ def test_one_wave_chunk_boundaries_and_short_tail():
         CO.atomic_one_wave(r0, r1, lockf, c, i, negs, alpha, st["stripe_rows"],
                            st["stripe_copies"], st["stripe2_rows"], st["stripe2_copies"])
         assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (n, _rel(g0, r0), _rel(g1, r1))
+
+
+@pytest.mark.parametrize("stripes", ["default", "two_tier"])
+def test_kernel_variants_same_values(stripes):
+    """the instances G2V_OPT_ATOMIC_TAILS / G2V_OPT_COPY_DEFER choose between
+     change only the instruction schedule: on one wave each
+    matches the restatement and they agree with each other to rounding"""
+    V, D, K, n, alpha = 40, 200, 5, 3000, 0.025
+    rng = np.random.RandomState(7)
+    syn0 = ((rng.rand(V, D) - 0.5) / D).astype(np.float32)
+    syn1 = ((rng.rand(V, D) - 0.5) / D * 0.1).astype(np.float32)
+    lockf = np.ones(V, np.float32)
+    c, i, negs = _examples(V, K, n, seed=11)
+    out = {}
+    for tails in (0, 1):
+        for defer in (0, 1):
+            e = E.SGNSEngine(V, D, K)
+            e.set_weights(syn0, syn1)
+            e.set_option(N.OPT_GRID, 1)
+            e.set_option(N.OPT_ACTIVE_WAVES, 1)
+            e.set_option(N.OPT_ATOMIC_TAILS, tails)
+            e.set_option(N.OPT_COPY_DEFER, defer)
+            for k, v in STRIPES[stripes].items():
+                e.set_option(k, v)
+            e.step_explicit(c, i, negs, alpha, mode=N.MODE_HOGWILD)
+            out[tails, defer] = e.get_weights()
+            st = e.read_stats()
+            e.close()
+    r0, r1 = syn0.copy(), syn1.copy()
+    CO.atomic_one_wave(r0, r1, lockf, c, i, negs, alpha, st["stripe_rows"], st["stripe_copies"],
+                       st["stripe2_rows"], st["stripe2_copies"])
+    base0, base1 = out[0, 1]  # the defaults
+    for key, (g0, g1) in out.items():
+        assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (key, _rel(g0, r0), _rel(g1, r1))
+        assert _rel(g0, base0) < 1e-6 and _rel(g1, base1) < 1e-6, (key, _rel(g0, base0),
+                                                                   _rel(g1, base1))
