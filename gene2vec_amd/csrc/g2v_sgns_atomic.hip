@@ -28,6 +28,7 @@ namespace g2v {
 // so each atomic wave-instruction adds 64 contiguous floats (256 B); the
 // row's buffer resource drops the lanes past D.
 constexpr int kStripeBatch = 7;
+constexpr int kDeferSlots = 3;
 constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
 
 template <int K, int NV>
@@ -41,9 +42,15 @@ struct ExRegs {
   // row); added to the main row once the main rows have landed (add_copies)
   float4 cs[K + 2][NV];
   bool cp[K + 2];
-  // DC: a striped row's last (up to kStripeBatch) copies, left in flight with
-  // the main rows and added to cs in copy order at add_copies
-  float4 dc[K + 2][kStripeBatch][NV];
+  // DC: the last (up to kStripeBatch) copies of the example's first
+  // kDeferSlots striped rows (slot s: the s-th striped row in row order), left
+  // in flight with the main rows and added to cs in copy order at add_copies;
+  // a later striped row's copies are all summed in load_example.  The slots,
+  // not one per row, keep
+  // the kernel at 2 waves per SIMD, so the sampler's waves can share the CUs
+  // (one slot per row took 306 registers: occupancy 1, and k_job_sample then
+  // waited for whole SGNS launches; profiles/r04/r04_bench_kernel_stats.csv)
+  float4 dc[kDeferSlots][kStripeBatch][NV];
 };
 
 // row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
@@ -168,6 +175,7 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
   // throughput a drained-copy design would have; values go stale)
   const int R1 = a.skip_copy_reads ? 0 : a.stripe_rows;
   const int R2 = a.skip_copy_reads ? 0 : a.stripe2_rows;
+  int nslot = 0;  // DC: the first kDeferSlots striped rows keep their last batch in flight
 #pragma unroll
   for (int d = 0; d <= K + 1; ++d) {
     const int t = d <= K ? x.tg[d] : x.input;
@@ -177,7 +185,9 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 #pragma unroll
     for (int v = 0; v < NV; ++v) x.cs[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
     const int C = t < R1 ? a.stripe_copies : a.stripe2_copies;
-    const int c_end = DC ? (C - 1 > kStripeBatch ? C - kStripeBatch : 1) : C;  // summed now
+    int c_end = C;  // copies [1, c_end) summed now
+    if (DC && nslot < kDeferSlots) c_end = C - 1 > kStripeBatch ? C - kStripeBatch : 1;
+    ++nslot;
     if (t < R1)
       add_stripes<NV>(x.cs[d], rs, t, tbl, R1, C, rowb, loff, c_end);
     else
@@ -185,10 +195,19 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
   }
   if constexpr (DC) {
 #pragma unroll
-    for (int d = 0; d <= K + 1; ++d) {
-      if (!x.cp[d]) continue;
-      const int t = d <= K ? x.tg[d] : x.input;
-      const int tbl = d <= K ? 1 : 0;
+    for (int s = 0; s < kDeferSlots; ++s) {
+      // the s-th striped row of the example (wave-uniform scalars)
+      int t = -1, tbl = 0, n = 0;
+#pragma unroll
+      for (int d = 0; d <= K + 1; ++d) {
+        if (!x.cp[d]) continue;
+        if (n == s) {
+          t = d <= K ? x.tg[d] : x.input;
+          tbl = d <= K ? 1 : 0;
+        }
+        ++n;
+      }
+      if (t < 0) continue;  // fewer striped rows: slot s unused (never read)
       const bool t1 = t < R1;
       const int C = t1 ? a.stripe_copies : a.stripe2_copies;
       const int rows = t1 ? R1 : R2 - R1;
@@ -200,7 +219,8 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
         const uint32_t base =
             c < C ? (uint32_t)((int)stripe_row(tbl, tt, c, rows, C) * rowb) : (uint32_t)kStripeOob;
 #pragma unroll
-        for (int v = 0; v < NV; ++v) x.dc[d][j][v] = bload4<0>(t1 ? rs : rs2, (int)(base + loff[v]));
+        for (int v = 0; v < NV; ++v)
+          x.dc[s][j][v] = bload4<0>(t1 ? rs : rs2, (int)(base + loff[v]));
       }
     }
   }
@@ -221,19 +241,24 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 // main rows have landed
 template <int K, int NV, bool DC = false>
 __device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
+  int n = 0;  // DC: row d's slot = the striped rows before it
 #pragma unroll
   for (int d = 0; d <= K + 1; ++d) {
     if (!x.cp[d]) continue;
     if constexpr (DC) {
 #pragma unroll
-      for (int j = 0; j < kStripeBatch; ++j)
+      for (int s = 0; s < kDeferSlots; ++s)
+        if (n == s)
 #pragma unroll
-        for (int v = 0; v < NV; ++v) {
-          x.cs[d][v].x += x.dc[d][j][v].x;
-          x.cs[d][v].y += x.dc[d][j][v].y;
-          x.cs[d][v].z += x.dc[d][j][v].z;
-          x.cs[d][v].w += x.dc[d][j][v].w;
-        }
+          for (int j = 0; j < kStripeBatch; ++j)
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+              x.cs[d][v].x += x.dc[s][j][v].x;
+              x.cs[d][v].y += x.dc[s][j][v].y;
+              x.cs[d][v].z += x.dc[s][j][v].z;
+              x.cs[d][v].w += x.dc[s][j][v].w;
+            }
+      ++n;
     }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
