@@ -148,7 +148,7 @@ struct g2v_ctx {
   int64_t stripe2_cap = 0;
   int atomic_overlap = 1;
   int atomic_tails = 0;  // G2V_OPT_ATOMIC_TAILS (measured slower than separate tails)
-  int copy_defer = 1;    // G2V_OPT_COPY_DEFER
+  int copy_defer = 0;    // G2V_OPT_COPY_DEFER (measured slower than the eager sum)
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int64_t debug_fail_merge = 0;  // G2V_OPT_DEBUG_FAIL_MERGE: fault injection

@@ -178,11 +178,13 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         (22 instead of 28 per example), 0 = one tail
  *                         instruction per row [0: one instruction over seven
  *                         rows measured 1.5-4 % slower, DESIGN.md 5d]
- *   G2V_OPT_COPY_DEFER    Hogwild kernel at D <= 256: 1 = a striped row's last
- *                         (up to 7) copies stay in flight with the main rows
+ *   G2V_OPT_COPY_DEFER    Hogwild kernel at D <= 256: 1 = the last (up to 7)
+ *                         copies of an example's first 3 striped rows stay
+ *                         in flight with the main rows
  *                         under the previous example's atomics and are summed
  *                         at first use, 0 = every copy is summed before the
- *                         main rows are requested (same values either way) [1]
+ *                         main rows are requested (same values either way)
+ *                         [0: 2-3.5 % slower in its 3-slot form, DESIGN.md 5d]
  *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the
  *                         n-th in-call merge of every g2v_train call fails
  *                         before its collective, as a rank that dies between

@@ -135,7 +135,7 @@ def test_kernel_variants_same_values(stripes):
     r0, r1 = syn0.copy(), syn1.copy()
     CO.atomic_one_wave(r0, r1, lockf, c, i, negs, alpha, st["stripe_rows"], st["stripe_copies"],
                        st["stripe2_rows"], st["stripe2_copies"])
-    base0, base1 = out[0, 1]  # the defaults
+    base0, base1 = out[0, 0]  # the defaults
     for key, (g0, g1) in out.items():
         assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (key, _rel(g0, r0), _rel(g1, r1))
         assert _rel(g0, base0) < 1e-6 and _rel(g1, base1) < 1e-6, (key, _rel(g0, base0),
