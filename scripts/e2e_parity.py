@@ -217,7 +217,7 @@ def main():
     summ = {}
     for key in ("loss", "heldin", "target_ratio", "auc_mean"):
         g, o = mean("gpu", key), mean("oracle", key)
-        ov = [r[key] for t, r in log["runs"].items() if t.startswith("oracle_seed")]
+        ov = [r[key] for t, r in log["runs"].items() if t.startswith("oracle_seed") and key in r]
         summ[key] = {"gpu": g, "oracle": o,
                      "gap": None if g is None or o is None else round((g - o) / o, 5),
                      "oracle_spread": round((max(ov) - min(ov)) / abs(np.mean(ov)), 5)
