@@ -75,7 +75,7 @@ def parse():
     p.add_argument("--negative", type=int, default=5)
     p.add_argument("--sample", type=float, default=1e-3)
     p.add_argument("--zipf", type=float, default=1.0)
-    p.add_argument("--avg-every-jobs", type=int, default=4096,
+    p.add_argument("--avg-every-jobs", type=int, default=3584,
                    help="replica merge cadence in jobs per rank (N>1; the CLI's default)")
     p.add_argument("--merge", choices=("touch", "mean"), default="touch",
                    help="replica merge rule (gene2vec_amd.distributed)")

@@ -236,9 +236,9 @@ def main(argv=None):
                         help="load every iteration's model back from the checkpoint just "
                              "written, as src/gene2vec.py:86 does (the kept in-memory model "
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
-    parser.add_argument("--merge-every-jobs", type=int, default=4096,
+    parser.add_argument("--merge-every-jobs", type=int, default=3584,
                         help="data-parallel replica merge cadence of the touch rule (gensim "
-                             "jobs per rank; 4096 = 7 merges per epoch at C3, DESIGN.md 7a)")
+                             "jobs per rank; 3584 = 7 merges per epoch at C3, DESIGN.md 7a)")
     parser.add_argument("--merge-rule", choices=("auto", "touch", "align", "mean"),
                         default="auto",
                         help="data-parallel replica merge rule: auto = touch every "

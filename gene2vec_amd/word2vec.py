@@ -296,7 +296,7 @@ def _load_npz(fname):
 # largest that kept 8 replicas within 1 % of one model on every measured metric
 # at C3's size (SGNS objective held-in / held-out, GGIPNN AUC, target function;
 # DESIGN.md section 7a, profiles/r03/replica_quality_c3*.json)
-DP_MERGE_EVERY_JOBS = 4096
+DP_MERGE_EVERY_JOBS = 3584
 # merge transport under torch.distributed: "auto" = libg2v over RCCL for nccl,
 # libg2v over the host collective for gloo; "torch" = torch-owned tables merged
 # by torch.distributed (the CLI's --merge-transport)

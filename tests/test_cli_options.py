@@ -19,11 +19,11 @@ def _parsed(argv):
 
 
 def test_cli_defaults_match_the_c3_gate():
-    """tests/test_gpu_c3_quality.py runs the CLI's defaults: a merge every 4,096
+    """tests/test_gpu_c3_quality.py runs the CLI's defaults: a merge every 3,584
     jobs and sharding from 125 M pairs per rank; the reference's own settings
     (src/gene2vec.py:57-63) stay the CLI's"""
     a = _parsed(["d", "o", "txt"])
-    assert a["merge_every_jobs"] == 4096 and a["dp_min_pairs_per_rank"] == 50_000_000
+    assert a["merge_every_jobs"] == 3584 and a["dp_min_pairs_per_rank"] == 50_000_000
     assert a["merge_rule"] == "auto"
     assert (a["dim"], a["negative"], a["window"], a["sample"], a["iters"], a["workers"]) == \
         (200, 5, 1, 1e-3, 10, 32)
@@ -41,16 +41,20 @@ def test_sample0_warns_about_the_target_function(capsys):
 
 
 def test_dp_merge_plan_by_shard_size():
-    """distributed.dp_merge_plan: touch every 4,096 jobs from 125 M pairs per
-    rank (C3, tests/test_gpu_c3_quality.py), align at 7 merges per epoch from
-    50 M (tests/test_gpu_c3_quality.py's 50 M gate); explicit rules keep the
-    cadence"""
+    """distributed.dp_merge_plan: touch every 3,584 jobs from 125 M pairs per
+    rank (C3, tests/test_gpu_c3_quality.py), touch at 7 merges per epoch from
+    80 M, align at 7 merges per epoch from 50 M (tests/test_gpu_c3_quality.py's
+    50 M gate); explicit rules keep the cadence"""
     from gene2vec_amd import distributed as Dd
-    assert Dd.dp_merge_plan(125_000_000) == ("touch", 4096)
+    assert Dd.dp_merge_plan(125_000_000) == ("touch", 3584)
     assert Dd.dp_merge_plan(1_000_000_000, 1024) == ("touch", 1024)
     # 50 M pairs = 10,000 jobs of 5,000 pairs -> every 1,429 jobs = 7 merges
     assert Dd.dp_merge_plan(50_000_000) == ("align", 1429)
-    rule, every = Dd.dp_merge_plan(80_000_000)
+    rule, every = Dd.dp_merge_plan(79_999_999)
     assert rule == "align" and -(-16_000 // every) == 7
+    rule, every = Dd.dp_merge_plan(80_000_000)
+    assert rule == "touch" and every == 2286 and -(-16_000 // every) == 7
+    assert Dd.dp_merge_plan(100_000_000) == ("touch", 2858)
+    assert Dd.dp_merge_plan(100_000_000, 1000) == ("touch", 1000)
     assert Dd.dp_merge_plan(50_000_000, 4096, "touch") == ("touch", 4096)
     assert Dd.dp_merge_plan(60_000_000, 333, "mean") == ("mean", 333)

@@ -3,7 +3,7 @@
 
 C3 = 8 ranks x 125 M pairs (1 B pairs), dim 200, neg 5, sample 1e-3, the
 reference's 10-iteration alpha sawtooth (src/gene2vec.py:67-92), replicas
-merged by libg2v's touch rule every 4,096 jobs (the CLI's
+merged by libg2v's touch rule every 3,584 jobs (the CLI's
 --merge-every-jobs default, 7 merges per epoch).  Here the 8 replicas run on
 ONE GPU through the in-process replica group (libg2v's merge kernels and
 in-call merges: the production merge path of distributed.ReplicaTrainer) and
@@ -17,9 +17,10 @@ Gate (north star: data-parallel quality within 1 % of one model): the
 manuscript target function (src/evaluation_target_function.py, pathways =
 the planted modules), the SGNS objective on training pairs (held-in) and on
 fresh pairs of the generator (held-out), each within 1 % of the one model's.
-From 125 M pairs per rank the CLI merges this way (distributed.dp_merge_plan);
-from 50 M, its --dp-min-pairs-per-rank default, it switches to the align rule
-at 7 merges per epoch, gated by the second test (below 50 M, DESIGN.md 7b, no
+From 125 M pairs per rank the CLI merges this way (distributed.dp_merge_plan;
+from 80 M the same rule at 7 merges per epoch); from 50 M, its
+--dp-min-pairs-per-rank default, it switches to the align rule at 7 merges
+per epoch, gated by the second test (below 50 M, DESIGN.md 7b, no
 measured rule holds the target function).  About 2 x 62 s of
 training plus the corpus and the scoring; progress goes to
 gpurun_out/c3_quality_progress.log."""
@@ -49,7 +50,7 @@ def _progress():
 def test_c3_eight_replicas_within_one_percent_of_one_model(tmp_path):
     from gene2vec_amd import replica_study as RQ
     say = _progress()
-    R, per, every = 8, 125_000_000, 4096
+    R, per, every = 8, 125_000_000, 3584
     st = RQ.Study(R, per, 24447, rep=3, modules=1000, p_in=0.5, zipf=1.0, iters=10)
     say(f"corpus: {st.n} pairs, V {st.V}")
     gmt = st.gmt(str(tmp_path / "modules.gmt"))
@@ -69,7 +70,7 @@ def test_c3_eight_replicas_within_one_percent_of_one_model(tmp_path):
           f"one model: " + ", ".join(f"{k} {rep[k]:.5f} vs {one[k]:.5f} ({gaps[k]:+.3%})"
                                      for k in one))
     assert same  # every replica holds the merged bits
-    assert merges == 7 * 10  # 25,000 jobs per rank per epoch, a merge every 4,096
+    assert merges == 7 * 10  # 25,000 jobs per rank per epoch, a merge every 3,584
     assert one["heldin"] < 0.5 * (st.K + 1) * np.log(2)  # trained, not noise
     assert one["target"] > 1.5  # modules closer than random pairs
     for k, g in gaps.items():

@@ -1,7 +1,7 @@
 """GPU: data-parallel merge machinery at the production cadence, reduced from
 C3: the SGNS objectives only.
 
-C3 = 8 ranks x 125 M pairs, a touch merge every 4,096 jobs (the default) =
+C3 = 8 ranks x 125 M pairs, a touch merge every 3,584 jobs (the default) =
 every 20.5 M pairs per rank, i.e. 7 merges per epoch.  Here a tenth of it: 8
 replicas on one GPU through the in-process group (libg2v's merge kernels and
 in-call merges, the production path of ReplicaTrainer), 8 x 12.5 M pairs of a
