@@ -329,7 +329,8 @@ MERGE_RULES = {"touch": 0, "mean": 1, "align": 2}  # == G2V_MERGE_TOUCH / _MEAN 
 #   80 M .. 125 M: touch at 7 merges per epoch (80 M: -0.97 %, where align at
 #       7 per epoch overshoots to +2.0 %)
 #   50 M .. 80 M: align at 7 merges per epoch (50 M, three runs: -0.18 ..
-#       +0.24 %, where touch reads -3.6 %); the second C3-quality test gates it
+#       +0.24 %, where touch reads -3.6 %; 65 M: +1.1 .. +1.4 %, touch -1.75 %);
+#       the second C3-quality test gates it at 50 M
 #   below 50 M no measured rule or cadence holds the target function (12.5 M:
 #       -2.6 % at best), so the CLI trains the corpus whole on every rank.
 # The SGNS objectives (held-in / held-out) and GGIPNN AUC stay within 0.6 % in
