@@ -78,42 +78,6 @@ def test_c3_eight_replicas_within_one_percent_of_one_model(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(900)
-def test_c3_second_corpus_within_one_percent(tmp_path):
-    """the default cadence on the second structured corpus it was derived on
-    (corpus B: Zipf 1.2 over 24,447 genes, 600 planted modules of
-    ~41 genes, 30 % of the pairs rewired into them, GGIPNN positives x3), the
-    C3 shard and metrics of the gate above.  Measured in round 4 at 3,584
-    jobs: target function -0.71 / -0.83 %, held-in -0.64 / -0.78 %, held-out
-    -0.09 / -0.21 % over two job-seed streams (the round-3 default of 4,096
-    read -1.1 % on the target function here)."""
-    from gene2vec_amd import distributed as Dd
-    from gene2vec_amd import replica_study as RQ
-    say = _progress()
-    R, per = 8, 125_000_000
-    st = RQ.Study(R, per, 24447, rep=3, modules=600, p_in=0.3, zipf=1.2, iters=10)
-    rule, every = Dd.dp_merge_plan(st.n / R)
-    assert (rule, every) == ("touch", 3584)
-    say(f"corpus B: {st.n} pairs, V {st.V}")
-    gmt = st.gmt(str(tmp_path / "modules.gmt"))
-    s0, s1 = st.train_single(1)
-    one = {"heldin": st.heldin(s0, s1), "heldout": st.heldout(s0, s1),
-           "target": RQ.target_of(s0, st.index2word, st.vc, gmt, st.D)["ratio"]}
-    r0, r1, merges, same = st.train_replicas(every)
-    rep = {"heldin": st.heldin(r0, r1), "heldout": st.heldout(r0, r1),
-           "target": RQ.target_of(r0, st.index2word, st.vc, gmt, st.D)["ratio"]}
-    gaps = {k: (rep[k] - one[k]) / one[k] for k in one}
-    say(f"corpus B: one {one} replicas {rep} merges {merges} gaps {gaps}")
-    print(f"C3 corpus B: {R} replicas x {per} pairs, touch merge every {every} jobs ({merges} "
-          "merges) vs one model: " + ", ".join(f"{k} {rep[k]:.5f} vs {one[k]:.5f} "
-                                              f"({gaps[k]:+.3%})" for k in one))
-    assert same and merges == 7 * 10
-    assert one["target"] > 1.5
-    for k, g in gaps.items():
-        assert abs(g) < 0.01, (k, one, rep)
-
-
-@pytest.mark.gpu
 @pytest.mark.timeout(600)
 def test_dp_50m_per_rank_align_within_one_percent(tmp_path):
     """the smallest shard the CLI trains data-parallel (--dp-min-pairs-per-rank
