@@ -324,8 +324,9 @@ MERGE_RULES = {"touch": 0, "mean": 1, "align": 2}  # == G2V_MERGE_TOUCH / _MEAN 
 # model through the reference's 10-iteration flow, C3's corpus shape; gaps of
 # the manuscript target function, the metric that moves):
 #   >= 125 M pairs per rank: touch every 3,584 jobs (7 merges per C3 epoch):
-#       +0.70 % on corpus A, -0.71 .. -0.83 % on corpus B (4,096 jobs, the same
-#       merge count: +0.3 / -1.1 %); tests/test_gpu_c3_quality.py gates A
+#       +0.70 % on corpus A, -0.71 .. -1.02 % on corpus B over four runs (4,096
+#       jobs, the same merge count: +0.3 / -1.1 %); tests/test_gpu_c3_quality.py
+#       gates A
 #   80 M .. 125 M: touch at 7 merges per epoch (80 M: -0.97 %, where align at
 #       7 per epoch overshoots to +2.0 %)
 #   50 M .. 80 M: align at 7 merges per epoch (50 M, three runs: -0.18 ..
