@@ -42,14 +42,15 @@ struct ExRegs {
   // row); added to the main row once the main rows have landed (add_copies)
   float4 cs[K + 2][NV];
   bool cp[K + 2];
-  // DC: the last (up to kStripeBatch) copies of the example's first
-  // kDeferSlots striped rows (slot s: the s-th striped row in row order), left
-  // in flight with the main rows and added to cs in copy order at add_copies;
-  // a later striped row's copies are all summed in load_example.  The slots,
-  // not one per row, keep
-  // the kernel at 2 waves per SIMD, so the sampler's waves can share the CUs
-  // (one slot per row took 306 registers: occupancy 1, and k_job_sample then
-  // waited for whole SGNS launches; profiles/r04/r04_bench_kernel_stats.csv)
+  // DC (G2V_OPT_COPY_DEFER, off by default: measured 2-3.5 % slower than the
+  // eager sum): the last (up to kStripeBatch) copies of the
+  // example's first kDeferSlots striped rows (slot s: the s-th striped row in
+  // row order), left in flight with the main rows and added to cs in copy
+  // order at add_copies; a later striped row's copies are all summed in
+  // load_example.  The slots, not one per row, keep the kernel at 2 waves per
+  // SIMD, so the sampler's waves can share the CUs (one slot per row took 306
+  // registers: occupancy 1, and k_job_sample then waited for whole SGNS
+  // launches; profiles/r04/r04a_bench_kernel_stats.csv)
   float4 dc[kDeferSlots][kStripeBatch][NV];
 };
 
@@ -154,11 +155,12 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
 // back by a full load latency (round 4 stamps).
 __device__ __forceinline__ uint64_t stamp_time();
 //
-// DC (NV = 1): a striped row's last min(C - 1, kStripeBatch) copies are not
-// waited for either: they are requested after every row's earlier copies have
-// been summed and before the main rows, and stay in flight with them (at
-// sample 0's 8 copies per row: all of them, so the prefetch waits for
-// nothing); add_copies adds them to cs in copy order, so the value is the same.
+// DC (NV = 1; an option, off by default): the last min(C - 1, kStripeBatch)
+// copies of the example's first kDeferSlots striped rows are not waited for
+// either: they are requested after every row's earlier copies have been
+// summed and before the main rows, and stay in flight with them (at sample
+// 0's 8 copies per row: all of them); add_copies adds them to cs in copy
+// order, so the value is the same.
 template <int K, int NV, bool STAMP = false, bool DC = false>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
                                              const int32_t* r, __amdgpu_buffer_rsrc_t r0,
@@ -360,9 +362,9 @@ __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
 // full 256-B atomic instructions, and the K + 2 rows' short tails (D - 192
 // floats each) go out together in ONE instruction, lane l adding element
 // 192 + l % (D - 192) of row l / (D - 192): 3 (K + 2) + 1 instructions per
-// example instead of 4 (K + 2).  The memory side sees the same requests; the
-// wave issues 6 fewer vector-memory instructions at K 5, and a wave's atomics
-// stall on its outstanding vector-memory operations (round 4 stamps,
+// example instead of 4 (K + 2).  The memory side sees the same requests and
+// the wave issues 6 fewer vector-memory instructions at K 5, but it measured
+// 1.5-4 % slower than separate tails (G2V_OPT_ATOMIC_TAILS, off by default;
 // DESIGN.md 5d)
 template <int K, int NV, int WR = 0, bool LOSS = false, bool TC = false, bool DC = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
