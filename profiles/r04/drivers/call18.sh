@@ -6,4 +6,4 @@ mkdir -p gpurun_out/r04c18
 timeout -k 10 300 python -u -m pytest -x -q --timeout 250 --timeout-method thread \
   tests/test_gpu_atomic_order.py tests/test_gpu_parity.py tests/test_gpu_loss.py \
   > gpurun_out/r04c18/tests.log 2>&1 &&
-bash scripts/r04/call9.sh
+bash profiles/r04/drivers/call9.sh

@@ -8,4 +8,4 @@ timeout -k 10 240 python -u scripts/stamp_segments.py --sample 0 --grid 162 --pa
 timeout -k 10 240 python -u scripts/stamp_segments.py --sample 1e-3 --pairs 20000000 \
   --arms production,stamped,notail,production_again,notail_again \
   --out gpurun_out/r04c2/stamps_c2.json > gpurun_out/r04c2/stamps_c2.log 2>&1 &&
-bash scripts/r04/quality1.sh
+bash profiles/r04/drivers/quality1.sh

@@ -7,4 +7,4 @@ timeout -k 10 600 python -u -m pytest -x -v -s --timeout 560 --timeout-method th
 rc=$?
 echo "c3 test rc $rc" >> gpurun_out/r04q1/c3_test.log
 [ $rc -le 1 ] || exit $rc
-bash scripts/r04/small_dp.sh
+bash profiles/r04/drivers/small_dp.sh
