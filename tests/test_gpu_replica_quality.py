@@ -2,21 +2,21 @@
 C3: the SGNS objectives only.
 
 C3 = 8 ranks x 125 M pairs, a touch merge every 3,584 jobs (the default) =
-every 20.5 M pairs per rank, i.e. 7 merges per epoch.  Here a tenth of it: 8
+every 17.9 M pairs per rank, i.e. 7 merges per epoch.  Here a tenth of it: 8
 replicas on one GPU through the in-process group (libg2v's merge kernels and
 in-call merges, the production path of ReplicaTrainer), 8 x 12.5 M pairs of a
 structureless Zipf corpus, a merge every 410 jobs (the same 7 merges per
 epoch), the reference's alpha sawtooth over 2 iterations, against one model
 trained on the same permuted pairs.  Gate: the SGNS objective on the training
 pairs (held-in) and on a fresh draw of the generator (held-out) within 1 % of
-the one model's (measured +0.04 % / -0.01 %) -- the merge converges.
+the one model's (measured +0.18 % / +0.09 %) -- the merge converges.
 
 This is NOT the north star's quality claim: at 12.5 M pairs per replica the
-manuscript target function of merged replicas lags one model by 8.4 % on a
-corpus with planted modules (5 M: -14 %, 50 M: -4.6 %), which
-is why the CLI does not shard below --dp-min-pairs-per-rank = 125 M.  The
-target function within 1 % is gated at C3's full size, 8 x 125 M pairs, by
-tests/test_gpu_c3_quality.py."""
+manuscript target function of merged replicas lags one model by 2.6-8 % on a
+corpus with planted modules whatever the rule and cadence,
+which is why the CLI does not shard below --dp-min-pairs-per-rank = 50 M.  The
+target function within 1 % is gated at C3's full size, 8 x 125 M pairs, and
+at 8 x 50 M pairs with the align plan by tests/test_gpu_c3_quality.py."""
 import zlib
 from concurrent.futures import ThreadPoolExecutor
 
