@@ -242,10 +242,9 @@ def main(argv=None):
     parser.add_argument("--merge-rule", choices=("auto", "touch", "align", "mean"),
                         default="auto",
                         help="data-parallel replica merge rule: auto = touch every "
-                             "--merge-every-jobs jobs from 125 M pairs per rank, align at 7 "
-                             "merges per epoch from 50 M (the settings measured within 1 %% of "
-                             "one model, DESIGN.md 7a/7b); an explicit rule uses "
-                             "--merge-every-jobs")
+                             "--merge-every-jobs jobs from 125 M pairs per rank, touch at 7 "
+                             "merges per epoch from 80 M, align at 7 merges per epoch from 50 M "
+                             "(DESIGN.md 7a/7b); an explicit rule uses --merge-every-jobs")
     parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
                         default="auto",
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "

@@ -20,7 +20,7 @@ def _parsed(argv):
 
 def test_cli_defaults_match_the_c3_gate():
     """tests/test_gpu_c3_quality.py runs the CLI's defaults: a merge every 3,584
-    jobs and sharding from 125 M pairs per rank; the reference's own settings
+    jobs from 125 M pairs per rank and sharding from 50 M; the reference's own settings
     (src/gene2vec.py:57-63) stay the CLI's"""
     a = _parsed(["d", "o", "txt"])
     assert a["merge_every_jobs"] == 3584 and a["dp_min_pairs_per_rank"] == 50_000_000
