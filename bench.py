@@ -86,6 +86,9 @@ def parse():
     p.add_argument("--sample-overlap", type=int, choices=(0, 1), default=None,
                    help="G2V_OPT_SAMPLE_OVERLAP (sampler of segment s+1 under segment s's "
                         "SGNS kernel; default: the library's)")
+    p.add_argument("--tail-store", type=int, default=0,
+                   help="G2V_OPT_TAIL_STORE: rows >= this take plain stores instead of "
+                        "atomics (experiment, DESIGN.md 5e; 0 = off, the default)")
     p.add_argument("--seg-jobs", type=int, default=0,
                    help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
@@ -112,11 +115,91 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="PMC bytes per example for roofline.traffic (default: the newest "
                         "profiles/**/traffic_r*.json of this workload measured on this kernel build)")
+    p.add_argument("--launch-probe", action="store_true",
+                   help="test hook: the ranks agree on the world over gloo and rank 0 prints "
+                        "{n_gpus, ranks} without touching a GPU (checks --gpus N's own launcher)")
     return p.parse_args()
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start ONE child
+    `python -m torch.distributed.run --nproc-per-node N bench.py <same argv>`
+    (one rank per GPU, rendezvous on 127.0.0.1), forward rank 0's JSON line
+    and return the child's exit status.  Called before anything imports torch
+    or touches a GPU: the parent only waits (no exec of a GPU process)."""
+    import signal
+    import subprocess
+    assert "torch" not in sys.modules, "the launcher must not initialise torch / the GPU"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node",
+           str(n), "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get(
+        "HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    # same process group: a timeout that kills this process's group ends the ranks too
+    child = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True)
+
+    def _stop(signum, _frame):
+        child.terminate()
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, _stop)
+    lines = []
+    for ln in child.stdout:  # ranks print progress on stderr; stdout carries the one line
+        if ln.startswith("{"):
+            lines.append(ln)
+        else:
+            sys.stderr.write(ln)
+    rc = child.wait()
+    if lines:
+        sys.stdout.write(lines[-1])
+        sys.stdout.flush()
+    if rc != 0:
+        print(f"bench.py: {n}-rank run failed (torch.distributed.run exit {rc})", file=sys.stderr)
+    return rc
+
+
+def launch_probe(world, rank):
+    """--launch-probe: the N ranks of a spawned run meet over gloo (CPU only)"""
+    if world == 1:
+        print(json.dumps({"probe": True, "n_gpus": 1, "rank_sum": 1, "ranks_expected_sum": 1}),
+              flush=True)
+        return
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"probe": True, "n_gpus": world, "rank_sum": int(t.item()),
+                          "ranks_expected_sum": world * (world + 1) // 2}), flush=True)
+    dist.destroy_process_group()
 
 
 def main():
     a = parse()
+    # the process shape, decided before torch is imported (no GPU touched yet):
+    # under a launcher WORLD_SIZE must be --gpus; without one, --gpus N > 1
+    # starts its own N-rank child run
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and a.gpus > 1:
+        sys.exit(launch_ranks(a.gpus))
+    if env_world is not None and int(env_world) != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={env_world} "
+                 "ranks; pass --gpus equal to --nproc-per-node")
+    if a.gpus < 1:
+        sys.exit("bench.py: --gpus must be >= 1")
+    if a.launch_probe:
+        launch_probe(int(env_world or 1), int(os.environ.get("RANK", "0")))
+        return
     # stdout carries exactly one JSON line: the libraries' own chatter (RCCL
     # prints its version banner from C on fd 1) goes to stderr until then
     sys.stdout.flush()
@@ -179,6 +262,8 @@ def main():
         eng.set_option(N.OPT_STRIPE2_COPIES, c2)
     if a.seg_jobs:
         eng.set_option(N.OPT_SEG_JOBS, a.seg_jobs)
+    if a.tail_store:
+        eng.set_option(N.OPT_TAIL_STORE, a.tail_store)
     if a.sample_overlap is not None:
         eng.set_option(N.OPT_SAMPLE_OVERLAP, a.sample_overlap)
     # a dedicated (non-default) stream: g2v kernels, RCCL all-reduces and the
@@ -287,16 +372,15 @@ def main():
     # examples per launch; a profile of another build is refused (traffic null)
     from gene2vec_amd.build import kernel_source_hash
     ksha = kernel_source_hash()
-    # the layout the timed launches actually used (g2v_stats: the per-call
-    # stability cap may lower the grid below set_vocab's, which also changes
-    # the default stripe tiers), not the options' nominal values
+    # the layout the timed launches actually used (g2v_stats): the grid and
+    # stripe tiers are set_vocab's; the stability cap only holds waves back
+    # inside a launch (waves_last_launch below)
     launch = {"grid_workgroups": st["sgns_grid"],
               "stripes": f"{st['stripe_rows']}x{st['stripe_copies']}",
               "stripes_tier2": (f"rows < {st['stripe2_rows']} x{st['stripe2_copies']}"
                                 if st["stripe2_copies"] > 1 else "off"),
-              # kernel variants chosen at launch (same sources, other instances)
-              "atomic_tails": eng.get_option(N.OPT_ATOMIC_TAILS),
-              "copy_defer": eng.get_option(N.OPT_COPY_DEFER)}
+              # cold rows written by plain stores (G2V_OPT_TAIL_STORE, 0 = off)
+              "tail_store": eng.get_option(N.OPT_TAIL_STORE)}
     cands = [a.traffic_json] if a.traffic_json else sorted(
         glob.glob(os.path.join(ROOT, "profiles", "**", "traffic_r*.json"), recursive=True),
         reverse=True)
@@ -460,6 +544,10 @@ def main():
                 "dim": D, "negative": K, "sample": a.sample, "window": 1,
                 "parallelism": f"dp{world}" + (f" + {merge_backend} {a.merge} merge"
                                                if world > 1 else "")},
+            # per-GPU rate beside the shard it trained: N = 1 trains the C2
+            # 100 M pairs without merges, N > 1 a 125 M-pair shard per rank
+            # with merges, so compare points of a 1 -> N curve per GPU AND shard
+            "value_per_gpu": round(value / world, 1), "pairs_per_gpu": n_pairs,
             "examples_per_s": round(total_examples / elapsed, 1),
             "effective_examples": total_examples,
             "roofline": roofline, "cpu_baseline": cpu, "quality": quality,

@@ -19,7 +19,7 @@ G2V_ENOMEM = -3
 G2V_ESTATE = -4
 G2V_ERANGE = -5
 G2V_ECOMM = -6
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 MODE_HOGWILD = 0
 MODE_SEQUENTIAL = 1
@@ -49,8 +49,7 @@ OPT_ACTIVE_WAVES = 15
 OPT_MERGE_BETA_MILLI = 16
 OPT_MERGE_GAMMA_MILLI = 17
 OPT_DEBUG_FAIL_MERGE = 18
-OPT_ATOMIC_TAILS = 19
-OPT_COPY_DEFER = 20
+OPT_TAIL_STORE = 21
 COLL_SUM = 0
 COLL_BCAST0 = 1
 BATCH_WORDS = 10000
@@ -150,6 +149,16 @@ SIGNATURES = {
 }
 
 _lib = None
+
+
+def use_library(path):
+    """Load `path` (e.g. build.ABLATIONS_LIB, the -DG2V_ABLATIONS build the
+    throughput-ablation scripts use) instead of libg2v.so; only before the
+    first call into the library"""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != LIB_PATH:
+        raise NativeLibraryError(f"{LIB_PATH} is already loaded")
+    LIB_PATH = os.path.abspath(path)
 
 
 def lib():

@@ -51,25 +51,35 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found (need ROCm for gfx950)")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+# the throughput-ablation build (G2V_OPT_DEBUG_WRITE 1, 3-7, 9):
+# the same sources with -DG2V_ABLATIONS, a library of its own that is never
+# shipped or loaded by the product (scripts load it with _native.use_library)
+ABLATIONS_LIB = os.path.join(HERE, "build", "libg2v_ablations.so")
+
+
+def _stale(lib=LIB) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, s) for s in SOURCES] + HEADERS + [__file__]
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile every translation unit in parallel (one hipcc per file), then link."""
-    if not force and not _stale():
-        return LIB
+def build(force: bool = False, verbose: bool = False, ablations: bool = False) -> str:
+    """Compile every translation unit in parallel (one hipcc per file), then link.
+    ablations=True: the -DG2V_ABLATIONS library (ABLATIONS_LIB) instead."""
+    out = ABLATIONS_LIB if ablations else LIB
+    if not force and not _stale(out):
+        return out
     from concurrent.futures import ThreadPoolExecutor
-    objdir = os.path.join(HERE, "build")
+    objdir = os.path.join(HERE, "build", "ablations") if ablations else os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              # IEEE semantics: every fused multiply-add in the kernels is explicit
              "-ffp-contract=off", "-munsafe-fp-atomics", "-pthread",
              "-I", os.path.join(ROOT, "include"), "-I", CSRC]
+    if ablations:
+        flags.append("-DG2V_ABLATIONS")
     objs = [os.path.join(objdir, u[2]) for u in UNITS]
 
     def compile_one(i):
@@ -91,17 +101,17 @@ def build(force: bool = False, verbose: bool = False) -> str:
         for err in ex.map(compile_one, range(len(UNITS))):
             if err and verbose:
                 print(err, file=sys.stderr)
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    print(build(force="--force" in sys.argv, verbose=True, ablations="--ablations" in sys.argv))
 
 
 EXAMPLES = os.path.join(os.path.dirname(HERE), "examples")

@@ -147,8 +147,7 @@ struct g2v_ctx {
   float* stripe2 = nullptr;
   int64_t stripe2_cap = 0;
   int atomic_overlap = 1;
-  int atomic_tails = 0;  // G2V_OPT_ATOMIC_TAILS (measured slower than separate tails)
-  int copy_defer = 0;    // G2V_OPT_COPY_DEFER (measured slower than the eager sum)
+  int tail_store = 0;  // G2V_OPT_TAIL_STORE: first row of the plain-store tail, 0 = off
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int64_t debug_fail_merge = 0;  // G2V_OPT_DEBUG_FAIL_MERGE: fault injection
@@ -670,10 +669,24 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       REQUIRE(value >= 0 && value <= 32, G2V_EINVAL, "stripe copies out of [0, 32]");
       c->stripe_copies = (int)value;  // explicit: no longer chosen from the grid
       return G2V_OK;
-    case G2V_OPT_DEBUG_WRITE:
-      REQUIRE(value >= 0 && value <= 9, G2V_EINVAL, "debug write mode out of [0, 9]");
+    case G2V_OPT_DEBUG_WRITE: {
+      // 2 (gather roof) and 8 (stamps) are compiled for the reference's shape
+      // only (negative 5, D <= 256); the other modes only into the ablation
+      // build (-DG2V_ABLATIONS).  Refused otherwise instead of silently
+      // running the production kernel.
+#ifdef G2V_ABLATIONS
+      const bool known = value >= 0 && value <= 9;
+#else
+      const bool known = value == 0 || value == 2 || value == 8;
+#endif
+      REQUIRE(known, G2V_EINVAL, "debug write mode %lld is not compiled into this library",
+              (long long)value);
+      REQUIRE(value == 0 || (c->K == 5 && c->nv == 1), G2V_EINVAL,
+              "debug write mode %lld needs negative 5 and vector_size <= 256 (have %d, %d)",
+              (long long)value, c->K, c->D);
       c->debug_write = (int)value;
       return G2V_OK;
+    }
     case G2V_OPT_ATOMIC_OVERLAP:
       REQUIRE(value == 0 || value == 1, G2V_EINVAL, "atomic overlap must be 0 or 1");
       c->atomic_overlap = (int)value;
@@ -705,13 +718,16 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
               "merge gamma (x1000) out of [1000, 16000]");
       c->merge_gamma = (float)value / 1000.0f;
       return G2V_OK;
-    case G2V_OPT_ATOMIC_TAILS:
-      REQUIRE(value == 0 || value == 1, G2V_EINVAL, "atomic tails must be 0 or 1");
-      c->atomic_tails = (int)value;
-      return G2V_OK;
-    case G2V_OPT_COPY_DEFER:
-      REQUIRE(value == 0 || value == 1, G2V_EINVAL, "copy defer must be 0 or 1");
-      c->copy_defer = (int)value;
+    case G2V_OPT_RETIRED_19:
+    case G2V_OPT_RETIRED_20:
+      return fail(G2V_EINVAL, "option %d was retired in ABI 5 (measured slower, DESIGN.md 5d)",
+                  key);
+    case G2V_OPT_TAIL_STORE:
+      REQUIRE(value >= 0 && value <= c->V, G2V_EINVAL, "tail store row %lld out of [0, V]",
+              (long long)value);
+      REQUIRE(value == 0 || (c->nv == 1 && c->K + 1 <= 8), G2V_EINVAL,
+              "tail stores need vector_size <= 256 and negative <= 7");
+      c->tail_store = (int)value;
       return G2V_OK;
     case G2V_OPT_DEBUG_FAIL_MERGE:
       REQUIRE(value >= 0, G2V_EINVAL, "debug fail merge < 0");
@@ -747,8 +763,7 @@ int g2v_get_option(g2v_ctx* c, int key, int64_t* out) {
     case G2V_OPT_MERGE_BETA_MILLI: *out = (int64_t)lrintf(c->merge_beta * 1000.0f); return G2V_OK;
     case G2V_OPT_MERGE_GAMMA_MILLI: *out = (int64_t)lrintf(c->merge_gamma * 1000.0f); return G2V_OK;
     case G2V_OPT_DEBUG_FAIL_MERGE: *out = c->debug_fail_merge; return G2V_OK;
-    case G2V_OPT_ATOMIC_TAILS: *out = c->atomic_tails; return G2V_OK;
-    case G2V_OPT_COPY_DEFER: *out = c->copy_defer; return G2V_OK;
+    case G2V_OPT_TAIL_STORE: *out = c->tail_store; return G2V_OK;
     default: return fail(G2V_EINVAL, "option key %d cannot be read", key);
   }
 }
@@ -1112,8 +1127,6 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.stripe_rows = striped ? srows : 0;
   s.stripe_copies = striped ? copies : 1;
   s.overlap = c->atomic_overlap;
-  s.tail_combine = c->debug_write == 0 ? c->atomic_tails : 0;
-  s.copy_defer = (c->debug_write == 0 || c->debug_write == 8) ? c->copy_defer : 0;
   s.active_waves = c->active_waves;
   s.queue = c->d_queue;
   int rc;
@@ -1143,6 +1156,10 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     }
   }
   s.stripe2 = c->stripe2;
+  // cold-row plain stores (G2V_OPT_TAIL_STORE), never on a striped row
+  s.tail_row = (c->tail_store > 0 && c->debug_write == 0)
+                   ? std::max(c->tail_store, std::max(s.stripe_rows, s.stripe2_rows))
+                   : 0x7fffffff;
   if (c->debug_write == 3 || c->debug_write == 4 || c->debug_write == 7) {
     const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
     const int64_t words = rows * c->ld * (c->debug_write == 3 ? 1 : 2);

@@ -92,8 +92,8 @@ struct SgnsArgs {
   int D;
   int V;
   int hot_rows;             // rows [0, hot_rows) are updated with float atomics
-  int debug_write;          // ablation: 0 atomics, 1 plain stores, 2 no writes,
-                            // 3 packed-f16 atomics into a scratch table
+  int debug_write;          // 0 production, 2 no table writes (gather roof), 8 stamps;
+                            // the -DG2V_ABLATIONS build adds 1, 3, 4, 5, 9
   const float* exp_table;   // [1000]
   // hot-row striping (k_sgns_atomic): rows [0, stripe_rows) of each table have
   // stripe_copies-1 extra copies; value = main + sum(copies), atomics spread
@@ -105,7 +105,7 @@ struct SgnsArgs {
   float* stripe2;
   int stripe2_rows;         // <= stripe_rows = off
   int stripe2_copies;
-  int skip_copy_reads;      // ablation (G2V_OPT_DEBUG_WRITE 6): readers ignore stripe copies
+  int skip_copy_reads;      // ablation build (G2V_OPT_DEBUG_WRITE 6/7): readers ignore copies
   int overlap;              // G2V_OPT_ATOMIC_OVERLAP
   int active_waves;         // G2V_OPT_ACTIVE_WAVES: waves per workgroup that train (1..4)
   unsigned int* queue;      // k_sgns_atomic chunk counter, zeroed before every launch
@@ -119,8 +119,8 @@ struct SgnsArgs {
   float cap_coef;           // p_tok_max x (K+1) x the launch's largest alpha
   float cap_budget;
   int* waves_out;           // the waves that trained (block 0 writes it)
-  int tail_combine;         // G2V_OPT_ATOMIC_TAILS (k_sgns_atomic TC)
-  int copy_defer;           // G2V_OPT_COPY_DEFER (k_sgns_atomic DC)
+  int tail_row;             // G2V_OPT_TAIL_STORE: rows >= this take plain stores
+                            // (k_sgns_atomic, repeat-free examples; >= V: none)
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])

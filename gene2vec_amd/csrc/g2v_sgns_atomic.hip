@@ -27,8 +27,13 @@ namespace g2v {
 // behind e+1's compute.  l1 and work are staged through LDS in element order
 // so each atomic wave-instruction adds 64 contiguous floats (256 B); the
 // row's buffer resource drops the lanes past D.
+//
+// Build variants: the production library compiles WR 0 (production), 2 (the
+// write-free gather roof bench.py measures) and 8 (s_memtime stamps,
+// scripts/stamp_segments.py).  The throughput ablations (WR 1, 3, 4, 5, 9 and
+// G2V_OPT_DEBUG_WRITE 6 / 7) exist only in the -DG2V_ABLATIONS build
+// (gene2vec_amd.build.build(ablations=True) -> build/libg2v_ablations.so).
 constexpr int kStripeBatch = 7;
-constexpr int kDeferSlots = 3;
 constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
 
 template <int K, int NV>
@@ -42,16 +47,6 @@ struct ExRegs {
   // row); added to the main row once the main rows have landed (add_copies)
   float4 cs[K + 2][NV];
   bool cp[K + 2];
-  // DC (G2V_OPT_COPY_DEFER, off by default: measured 2-3.5 % slower than the
-  // eager sum): the last (up to kStripeBatch) copies of the
-  // example's first kDeferSlots striped rows (slot s: the s-th striped row in
-  // row order), left in flight with the main rows and added to cs in copy
-  // order at add_copies; a later striped row's copies are all summed in
-  // load_example.  The slots, not one per row, keep the kernel at 2 waves per
-  // SIMD, so the sampler's waves can share the CUs (one slot per row took 306
-  // registers: occupancy 1, and k_job_sample then waited for whole SGNS
-  // launches; profiles/r04/r04a_bench_kernel_stats.csv)
-  float4 dc[kDeferSlots][kStripeBatch][NV];
 };
 
 // row t of table tbl (0 = syn0, 1 = syn1neg) as this lane's float4 column(s):
@@ -77,17 +72,14 @@ __device__ __forceinline__ void load_main(float4 (&o)[NV], __amdgpu_buffer_rsrc_
 template <int NV>
 __device__ __forceinline__ void add_stripes(float4 (&o)[NV], __amdgpu_buffer_rsrc_t rs, int t,
                                             int tbl, int rows, int C, int rowb,
-                                            const uint32_t (&loff)[NV], int c_end = -1) {
-  // copies [1, c_end) (default: all C - 1 of them)
-  if (c_end < 0) c_end = C;
-  for (int c0 = 1; c0 < c_end; c0 += kStripeBatch) {
+                                            const uint32_t (&loff)[NV]) {
+  for (int c0 = 1; c0 < C; c0 += kStripeBatch) {
     float4 q[kStripeBatch][NV];
 #pragma unroll
     for (int j = 0; j < kStripeBatch; ++j) {
       const int c = c0 + j;
       const uint32_t base =
-          c < c_end ? (uint32_t)((int)stripe_row(tbl, t, c, rows, C) * rowb)
-                    : (uint32_t)kStripeOob;
+          c < C ? (uint32_t)((int)stripe_row(tbl, t, c, rows, C) * rowb) : (uint32_t)kStripeOob;
 #pragma unroll
       for (int v = 0; v < NV; ++v) q[j][v] = bload4<0>(rs, (int)(base + loff[v]));
     }
@@ -113,8 +105,8 @@ __device__ __forceinline__ int wrap_copy(int c, int C) {
 }
 
 // destination of an atomic delta for row t of table tbl: the main row or the
-// stripe copy (craw mod copies) of its tier (WR 4, ablation: the same rows of
-// a scratch table the kernel never reads).  Byte offsets in 32 bits:
+// stripe copy (craw mod copies) of its tier (WR 4, ablation build: the same
+// rows of a scratch table the kernel never reads).  Byte offsets in 32 bits:
 // g2v_create caps a table below 2 GiB (the buffer offset range) and the
 // stripe buffers below 1 GiB, so a row's offset is one scalar multiply.
 template <int WR = 0>
@@ -130,12 +122,14 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
     return reinterpret_cast<float*>(reinterpret_cast<char*>(a.stripe2) + (uint32_t)(sr * rowb));
   }
   const int c = wrap_copy(craw, a.stripe_copies);
+#ifdef G2V_ABLATIONS
   if (WR == 4) {
     const int64_t nrow = (int64_t)a.V + (int64_t)(a.stripe_copies - 1) * a.stripe_rows;
     const int64_t rr =
         (c == 0 || t >= a.stripe_rows) ? t : a.V + (int64_t)(c - 1) * a.stripe_rows + t;
     return reinterpret_cast<float*>(a.dbg16) + (tbl * nrow + rr) * a.ld;
   }
+#endif
   if (c == 0 || t >= a.stripe_rows)
     return reinterpret_cast<float*>(reinterpret_cast<char*>(tbl ? a.wr1 : a.wr0) +
                                     (uint32_t)(t * rowb));
@@ -154,14 +148,7 @@ __device__ __forceinline__ float* upd_row(const SgnsArgs& a, int tbl, int t, int
 // for all of them before the first copy sum) held every example's atomics
 // back by a full load latency (round 4 stamps).
 __device__ __forceinline__ uint64_t stamp_time();
-//
-// DC (NV = 1; an option, off by default): the last min(C - 1, kStripeBatch)
-// copies of the example's first kDeferSlots striped rows are not waited for
-// either: they are requested after every row's earlier copies have been
-// summed and before the main rows, and stay in flight with them (at sample
-// 0's 8 copies per row: all of them); add_copies adds them to cs in copy
-// order, so the value is the same.
-template <int K, int NV, bool STAMP = false, bool DC = false>
+template <int K, int NV, bool STAMP = false>
 __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a,
                                              const int32_t* r, __amdgpu_buffer_rsrc_t r0,
                                              __amdgpu_buffer_rsrc_t r1, __amdgpu_buffer_rsrc_t rs,
@@ -173,11 +160,15 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
   x.alpha = __int_as_float(__builtin_amdgcn_readfirstlane(r[2]));
 #pragma unroll
   for (int d = 0; d < K; ++d) x.tg[d + 1] = __builtin_amdgcn_readfirstlane(r[3 + d]);
-  // ablation 6 (G2V_OPT_DEBUG_WRITE): copies are written but not read (the
+#ifdef G2V_ABLATIONS
+  // ablation 6 / 7 (G2V_OPT_DEBUG_WRITE): copies are written but not read (the
   // throughput a drained-copy design would have; values go stale)
   const int R1 = a.skip_copy_reads ? 0 : a.stripe_rows;
   const int R2 = a.skip_copy_reads ? 0 : a.stripe2_rows;
-  int nslot = 0;  // DC: the first kDeferSlots striped rows keep their last batch in flight
+#else
+  const int R1 = a.stripe_rows;
+  const int R2 = a.stripe2_rows;
+#endif
 #pragma unroll
   for (int d = 0; d <= K + 1; ++d) {
     const int t = d <= K ? x.tg[d] : x.input;
@@ -186,45 +177,10 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
     if (!x.cp[d]) continue;
 #pragma unroll
     for (int v = 0; v < NV; ++v) x.cs[d][v] = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int C = t < R1 ? a.stripe_copies : a.stripe2_copies;
-    int c_end = C;  // copies [1, c_end) summed now
-    if (DC && nslot < kDeferSlots) c_end = C - 1 > kStripeBatch ? C - kStripeBatch : 1;
-    ++nslot;
     if (t < R1)
-      add_stripes<NV>(x.cs[d], rs, t, tbl, R1, C, rowb, loff, c_end);
+      add_stripes<NV>(x.cs[d], rs, t, tbl, R1, a.stripe_copies, rowb, loff);
     else
-      add_stripes<NV>(x.cs[d], rs2, t - R1, tbl, R2 - R1, C, rowb, loff, c_end);
-  }
-  if constexpr (DC) {
-#pragma unroll
-    for (int s = 0; s < kDeferSlots; ++s) {
-      // the s-th striped row of the example (wave-uniform scalars)
-      int t = -1, tbl = 0, n = 0;
-#pragma unroll
-      for (int d = 0; d <= K + 1; ++d) {
-        if (!x.cp[d]) continue;
-        if (n == s) {
-          t = d <= K ? x.tg[d] : x.input;
-          tbl = d <= K ? 1 : 0;
-        }
-        ++n;
-      }
-      if (t < 0) continue;  // fewer striped rows: slot s unused (never read)
-      const bool t1 = t < R1;
-      const int C = t1 ? a.stripe_copies : a.stripe2_copies;
-      const int rows = t1 ? R1 : R2 - R1;
-      const int tt = t1 ? t : t - R1;
-      const int c_beg = C - 1 > kStripeBatch ? C - kStripeBatch : 1;
-#pragma unroll
-      for (int j = 0; j < kStripeBatch; ++j) {
-        const int c = c_beg + j;
-        const uint32_t base =
-            c < C ? (uint32_t)((int)stripe_row(tbl, tt, c, rows, C) * rowb) : (uint32_t)kStripeOob;
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-          x.dc[s][j][v] = bload4<0>(t1 ? rs : rs2, (int)(base + loff[v]));
-      }
-    }
+      add_stripes<NV>(x.cs[d], rs2, t - R1, tbl, R2 - R1, a.stripe2_copies, rowb, loff);
   }
   if (STAMP) *t_copies = stamp_time();  // copies summed (diagnostic build)
   load_main<NV>(x.l1, r0, x.input, rowb, loff);
@@ -241,27 +197,11 @@ __device__ __forceinline__ void load_example(ExRegs<K, NV>& x, const SgnsArgs& a
 
 // a striped row's value = main + (its copies summed in copy order), once the
 // main rows have landed
-template <int K, int NV, bool DC = false>
+template <int K, int NV>
 __device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
-  int n = 0;  // DC: row d's slot = the striped rows before it
 #pragma unroll
   for (int d = 0; d <= K + 1; ++d) {
     if (!x.cp[d]) continue;
-    if constexpr (DC) {
-#pragma unroll
-      for (int s = 0; s < kDeferSlots; ++s)
-        if (n == s)
-#pragma unroll
-          for (int j = 0; j < kStripeBatch; ++j)
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-              x.cs[d][v].x += x.dc[s][j][v].x;
-              x.cs[d][v].y += x.dc[s][j][v].y;
-              x.cs[d][v].z += x.dc[s][j][v].z;
-              x.cs[d][v].w += x.dc[s][j][v].w;
-            }
-      ++n;
-    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       float4& o = d <= K ? x.rw[d][v] : x.l1[v];
@@ -273,15 +213,15 @@ __device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
   }
 }
 
-// WR (debug ablation only): 0 atomics (production), 1 same-shape plain stores,
-// 2 no table writes, 3 packed-f16 atomics into a scratch table (half the atomic
-// bytes, tables never written: a throughput probe), 4 the production f32
-// atomics into that scratch table (tables never written), 5 production atomics
-// on syn1neg only, syn0 never written (the ceiling of any syn0-side combining),
-// 8 production with s_memtime stamps per loop segment (diagnostic build),
-// 9 production without each row's last atomic instruction (elements 192..255
-// at D <= 256: a throughput probe of the per-wave instruction count; breaks
-// training)
+// WR: 0 atomics (production), 2 no table writes (the gather roof), 8
+// production with s_memtime stamps per loop segment (diagnostic build); in the
+// -DG2V_ABLATIONS build also 1 same-shape plain stores, 3 packed-f16 atomics
+// into a scratch table (half the atomic bytes, tables never written: a
+// throughput probe), 4 the production f32 atomics into that scratch table
+// (tables never written), 5 production atomics on syn1neg only, syn0 never
+// written (the ceiling of any syn0-side combining), 9 production without each
+// row's last atomic instruction (elements 192..255 at D <= 256: a throughput
+// probe of the per-wave instruction count; breaks training)
 //
 // One row's delta coef * src[0, D) as a FIXED 4 * NV wave-instructions: the
 // buffer resource spans the row's D floats, so lanes past D (and every lane of
@@ -290,19 +230,25 @@ __device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
 // the compiler wait for the next example's row loads with vmcnt(#atomics)
 // instead of draining this example's atomics (vmcnt(0)) -- atomics retire in
 // the background while the wave computes.
-template <int NV, int WR, int NI = 4 * NV>
-__device__ __forceinline__ void emit_row(float* row, bool live, int D, const float (&src)[4 * NV],
-                                         float coef, int lane) {
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(float* row, bool live, int D) {
   // row and live are wave-uniform; say so, or the compiler waterfalls the resource
   const uint64_t pa = reinterpret_cast<uint64_t>(row);
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)pa);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(pa >> 32));
   const int nrec = __builtin_amdgcn_readfirstlane(live ? D * 4 : 0);
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-      reinterpret_cast<float*>(((uint64_t)hi << 32) | lo), (short)0, nrec, 0x00020000);
+  return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<float*>(((uint64_t)hi << 32) | lo),
+                                           (short)0, nrec, 0x00020000);
+}
+
+template <int NV, int WR>
+__device__ __forceinline__ void emit_row(float* row, bool live, int D, const float (&src)[4 * NV],
+                                         float coef, int lane) {
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row, live, D);
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
+  for (int i = 0; i < 4 * NV; ++i) {
+#ifdef G2V_ABLATIONS
     if (WR == 9 && i == 4 * NV - 1) continue;  // ablation: no tail instruction
+#endif
     const int off = (64 * i + lane) * 4;
     const float v = coef * src[i];
     if (WR == 0 || WR == 4 || WR == 5 || WR == 8 || WR == 9)
@@ -310,6 +256,25 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
     else if (WR == 1)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
   }
+}
+
+// G2V_OPT_TAIL_STORE (experiment; off by default): a cold row
+// (index >= a.tail_row, never striped) of a repeat-free example is written
+// with plain stores of its new value, the element-order row val[0, 4 NV),
+// instead of float atomics of the delta: the same 4 NV wave-instructions of
+// 256 contiguous bytes (so the loop head's vmcnt count is the same on both
+// paths), write-through (sc1: the line leaves the writer's L2, so a later read
+// on that XCD fetches the memory side's copy).  gensim's own Hogwild
+// read-modify-write, with the lost updates that implies when another wave
+// wrote the row between this wave's read and its store.
+template <int NV>
+__device__ __forceinline__ void store_row(float* row, bool live, int D, const float (&val)[4 * NV],
+                                          int lane) {
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row, live, D);
+#pragma unroll
+  for (int i = 0; i < 4 * NV; ++i)
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val[i]), r, (64 * i + lane) * 4, 0,
+                                          Pol<kPolWt>::st);
 }
 
 // LOSS ([ext] compute_loss): each wave keeps a float32 partial of the
@@ -328,6 +293,9 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 // instructions per row update, most of them address arithmetic)
 __device__ __forceinline__ float uniform_f(float x) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(x)));
+}
+__device__ __forceinline__ bool uniform_b(bool x) {
+  return __builtin_amdgcn_readfirstlane((int)x) != 0;
 }
 
 // In-kernel stamps (WR 8 only; cdna_hip_programming.md 7 "In-kernel stamps"):
@@ -357,26 +325,22 @@ __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
   return (int64_t)__builtin_amdgcn_readfirstlane(v);
 }
 
-// TC (tail combine, NV = 1 and 192 < D <= 192 + 64 / (K + 2): the
-// reference's dim 200 with K 5): every row sends its first 192 elements as 3
-// full 256-B atomic instructions, and the K + 2 rows' short tails (D - 192
-// floats each) go out together in ONE instruction, lane l adding element
-// 192 + l % (D - 192) of row l / (D - 192): 3 (K + 2) + 1 instructions per
-// example instead of 4 (K + 2).  The memory side sees the same requests and
-// the wave issues 6 fewer vector-memory instructions at K 5, but it measured
-// 1.5-4 % slower than separate tails (G2V_OPT_ATOMIC_TAILS, off by default;
-// DESIGN.md 5d)
-template <int K, int NV, int WR = 0, bool LOSS = false, bool TC = false, bool DC = false>
+// tail stores stage the new syn1neg rows in LDS: NV = 1 and K + 1 <= kTailMaxRows
+constexpr int kTailMaxRows = 8;
+template <int K, int NV>
+constexpr bool tail_ok() { return NV == 1 && K + 1 <= kTailMaxRows; }
+
+template <int K, int NV, int WR = 0, bool LOSS = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
-  static_assert(!TC || (NV == 1 && WR == 0), "tail combine: production kernel, D <= 256");
-  static_assert(!DC || NV == 1, "deferred copies: D <= 256");
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
   constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
+  constexpr bool TS = WR == 0 && tail_ok<K, NV>();  // tail stores compiled in
   __shared__ float s_lut[kExpTableSize];
   __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
   __shared__ float s_wk[W][256 * NV];
+  __shared__ float s_tl[W][TS ? NT * 256 : 1];  // tail rows' new values (TS)
   __shared__ int32_t s_rec[W][kChunk * RS];  // the wave's chunk of records
   __shared__ float s_lf[W][kChunk];          // lockf[input] per record of the chunk
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
@@ -420,22 +384,18 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
                                      (a.stripe2_rows - a.stripe_rows) * a.ld * 4
                                : 0);
   const int rowb = (int)a.ld * 4;
+  // first cold row taking plain stores (V or more: none; run_sgns keeps it
+  // past both stripe tiers)
+  const int tail_row = TS ? a.tail_row : 0x7fffffff;
   float* s1 = s_l1[wid];
   float* sw = s_wk[wid];
+  float* stl = s_tl[wid];
   int32_t* sr = s_rec[wid];
   float* slf = s_lf[wid];
   uint32_t loff[NV];  // this lane's byte offset in a row, out of range past D
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     loff[v] = (lane + 64 * v) < a.nvec ? (uint32_t)(lane * 16 + 1024 * v) : kLaneOob;
-  // TC: this lane's row (0..K: syn1neg targets, K+1: syn0) and element of the
-  // combined tail instruction; rows past K+1 send nothing
-  int tc_row = NT + 1, tc_el = 0;
-  if (TC) {
-    const int T = D - 192;
-    tc_row = lane / T;
-    tc_el = 192 + lane - tc_row * T;
-  }
 
   // WR 8: cycle sums per segment (see g2v_debug_stamps), wave-uniform scalars
   constexpr int kAtomicsPerExample = 4 * NV * (NT + 1);  // emit_row's fixed count
@@ -464,7 +424,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
     int cbase = (int)(e_beg % (int64_t)a.stripe_copies);
     float lsum = 0.f;
     ExRegs<K, NV> x;
-    load_example<K, NV, false, DC>(x, a, sr, r0, r1, rs, rs2, rowb, loff);
+    load_example<K, NV>(x, a, sr, r0, r1, rs, rs2, rowb, loff);
     // drain here, so the loop head only waits on the back edge's count
     // (vmcnt(#atomics of the previous example)); without it the two incoming
     // paths merge to vmcnt(0), which also waits for the previous atomics
@@ -482,7 +442,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         ++n_ex;
       }
       // ---- compute example e ------------------------------------------------
-      add_copies<K, NV, DC>(x);
+      add_copies<K, NV>(x);
       double pd[NT], dot[NT];
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
@@ -545,6 +505,15 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
             work[v].y = __fmaf_rn(gg, x.rw[d][v].y, work[v].y);
             work[v].z = __fmaf_rn(gg, x.rw[d][v].z, work[v].z);
             work[v].w = __fmaf_rn(gg, x.rw[d][v].w, work[v].w);
+          }
+          if (TS && x.tg[d] >= tail_row) {
+            // the cold row's new value, staged in element order for store_row
+            float4 nw;
+            nw.x = __fmaf_rn(gg, x.l1[0].x, x.rw[d][0].x);
+            nw.y = __fmaf_rn(gg, x.l1[0].y, x.rw[d][0].y);
+            nw.z = __fmaf_rn(gg, x.l1[0].z, x.rw[d][0].z);
+            nw.w = __fmaf_rn(gg, x.l1[0].w, x.rw[d][0].w);
+            *reinterpret_cast<float4*>(stl + d * 256 + lane * 4) = nw;
           }
           g[d] = gg;
           live[d] = true;
@@ -643,8 +612,8 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
       uint64_t tmain = ts;
       if (e + 1 < e_end)
-        load_example<K, NV, WR == 8, DC>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff,
-                                         &tmain);
+        load_example<K, NV, WR == 8>(x, a, sr + (q + 1) * RS, r0, r1, rs, rs2, rowb, loff,
+                                     &tmain);
       if (WR == 8) sub[3] += tmain - ts;
       if (WR == 8) {
         const uint64_t t = stamp_time();
@@ -653,6 +622,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
 
       // ---- atomics of example e -----------------------------------------------
+#ifdef G2V_ABLATIONS
       if (WR == 3) {
         typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
         const int hw = (int)(a.ld >> 1);
@@ -681,40 +651,37 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         cbase = cbase + 1 == a.stripe_copies ? 0 : cbase + 1;
         continue;
       }
-      // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work
-      if constexpr (TC) {
-        uint64_t tp = 0;  // this lane's tail destination, coefficient, liveness
-        float tcf = 0.f;
-        bool tok = false;
-#pragma unroll
-        for (int d = 0; d <= NT; ++d) {
-          float* row = d < NT ? upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb)
-                              : upd_row<WR>(a, 0, input, cbase + NT, rowb);
-          const bool lv = d < NT ? live[d] : any;
-          const float cf = d < NT ? g[d] : lf;
-          emit_row<NV, WR, 3>(row, lv, D, d < NT ? v1 : vw, cf, lane);
-          // lanes past row K+1 ride on the syn0 row's tail with a zero
-          if (tc_row == d || (d == NT && tc_row > NT)) {
-            tp = reinterpret_cast<uint64_t>(row);
-            tcf = cf;
-            tok = lv && tc_row <= NT;
-          }
-        }
-        const float tv = (tc_row < NT ? s1 : sw)[tc_el];
-        // unconditional (a skipped row's lanes add +0.0 to its tail): an
-        // exec-skip branch here would make the compiler wait for one of these
-        // atomics at the next example's first use of its rows
-        __builtin_amdgcn_global_atomic_fadd_f32(reinterpret_cast<float*>(tp) + tc_el,
-                                                tok ? tcf * tv : 0.0f);
-      } else {
+#endif
+      // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work.
+      // A row stored instead (G2V_OPT_TAIL_STORE) still issues its 4 NV
+      // atomics, dropped by an empty resource, and THEN its stores: every
+      // path issues at least the same 4 NV (K + 2) instructions after the
+      // next example's loads, so the loop head keeps waiting with
+      // vmcnt(#atomics) (an if / else of stores or atomics is lowered to two
+      // triangles, and the path through neither made it wait with vmcnt(0))
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
-        emit_row<NV, WR>(upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb),
-                         live[d], D, v1, g[d], lane);
+        float* row = upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb);
+        const bool st = uniform_b(TS && !rep && tg[d] >= tail_row);
+        emit_row<NV, WR>(row, live[d] && !st, D, v1, g[d], lane);
+        if (st) {
+          float val[4 * NV];
+#pragma unroll
+          for (int i = 0; i < 4 * NV; ++i) val[i] = stl[d * 256 + 64 * i + lane];
+          store_row<NV>(row, live[d], D, val, lane);
+        }
         if (WR == 8 && d == 3) sub[2] += stamp_time() - ts;  // 16 atomics issued
       }
-      emit_row<NV, WR>(upd_row<WR>(a, 0, input, cbase + NT, rowb),
-                       any && WR != 5, D, vw, lf, lane);
+      {
+        float* row = upd_row<WR>(a, 0, input, cbase + NT, rowb);
+        const bool st = uniform_b(TS && input >= tail_row);
+        emit_row<NV, WR>(row, any && !st && WR != 5, D, vw, lf, lane);
+        if (st) {
+          float val[4 * NV];
+#pragma unroll
+          for (int i = 0; i < 4 * NV; ++i) val[i] = __fmaf_rn(lf, vw[i], v1[i]);
+          store_row<NV>(row, any, D, val, lane);
+        }
       }
       __builtin_amdgcn_wave_barrier();
       if (WR == 8) acc[4] += stamp_time() - ts;
@@ -745,16 +712,27 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #define G2V_CAT2(a, b) a##b
 #define G2V_CAT(a, b) G2V_CAT2(a, b)
 
+// the instance a launch runs (run_sgns has already refused a debug mode this
+// shape does not compile: g2v_set_option, G2V_OPT_DEBUG_WRITE)
 hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int grid,
                                                  hipStream_t st) {
 #if G2V_K == 5
-  // ablation builds (G2V_OPT_DEBUG_WRITE), K = 5 / D <= 256 only
+  // the gather roof and the stamped diagnostic build, K = 5 / D <= 256 only
+  if (nv == 1 && a.debug_write == 2) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 8) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+#ifdef G2V_ABLATIONS
   if (nv == 1 && a.debug_write == 1) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 1>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
-  if (nv == 1 && a.debug_write == 2) {
-    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 2>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+  if (nv == 1 && a.debug_write == 3) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 3>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
   if (nv == 1 && a.debug_write == 4) {
@@ -765,53 +743,12 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 5>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
-  if (nv == 1 && a.debug_write == 3) {
-    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 3>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
-    return hipGetLastError();
-  }
-  if (nv == 1 && a.debug_write == 8) {
-    if (a.copy_defer)
-      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8, false, false, true>), dim3(grid),
-                         dim3(kSgnsThreads), 0, st, a);
-    else
-      hipLaunchKernelGGL((k_sgns_atomic<5, 1, 8>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
-    return hipGetLastError();
-  }
   if (nv == 1 && a.debug_write == 9) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 9>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
 #endif
-#if G2V_K == 5
-  // the reference's shape (dim 200, negative 5): combined row tails
-  if (nv == 1 && a.tail_combine && a.D > 192 && (a.D - 192) * (G2V_K + 2) <= 64) {
-    if (a.copy_defer) {
-      if (a.compute_loss)
-        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, true, true, true>), dim3(grid),
-                           dim3(kSgnsThreads), 0, st, a);
-      else
-        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, false, true, true>), dim3(grid),
-                           dim3(kSgnsThreads), 0, st, a);
-    } else {
-      if (a.compute_loss)
-        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, true, true>), dim3(grid), dim3(kSgnsThreads),
-                           0, st, a);
-      else
-        hipLaunchKernelGGL((k_sgns_atomic<5, 1, 0, false, true>), dim3(grid), dim3(kSgnsThreads),
-                           0, st, a);
-    }
-    return hipGetLastError();
-  }
 #endif
-  if (nv == 1 && a.copy_defer) {
-    if (a.compute_loss)
-      hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true, false, true>), dim3(grid),
-                         dim3(kSgnsThreads), 0, st, a);
-    else
-      hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, false, false, true>), dim3(grid),
-                         dim3(kSgnsThreads), 0, st, a);
-    return hipGetLastError();
-  }
   if (a.compute_loss) {
     if (nv == 1)
       hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true>), dim3(grid), dim3(kSgnsThreads), 0, st,

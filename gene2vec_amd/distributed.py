@@ -329,16 +329,18 @@ MERGE_RULES = {"touch": 0, "mean": 1, "align": 2}  # == G2V_MERGE_TOUCH / _MEAN 
 #       gates A
 #   80 M .. 125 M: touch at 7 merges per epoch (80 M: -0.97 %, where align at
 #       7 per epoch overshoots to +2.0 %)
-#   50 M .. 80 M: align at 7 merges per epoch (50 M, three runs: -0.18 ..
-#       +0.24 %, where touch reads -3.6 %; 65 M: +1.1 .. +1.4 %, touch -1.75 %);
-#       the second C3-quality test gates it at 50 M
-#   below 50 M no measured rule or cadence holds the target function (12.5 M:
-#       -2.6 % at best), so the CLI trains the corpus whole on every rank.
+#   below 80 M the CLI trains the corpus whole on every rank by default
+#       (DP_MIN_PAIRS, --dp-min-pairs-per-rank): no rule holds 1 %
+#       across 50 M .. 80 M (align, the plan there when a user lowers the
+#       threshold: 50 M -0.18 .. +0.24 % over three runs, gated by the second
+#       C3-quality test; 65 M +1.1 .. +1.4 %; 80 M +2.0 %; touch -3.6 / -1.75
+#       / -0.97 %), and below 50 M nothing measured holds it (12.5 M: -2.6 %
+#       at best).
 # The SGNS objectives (held-in / held-out) and GGIPNN AUC stay within 0.6 % in
 # every one of these arms.
 DP_TOUCH_MIN_PAIRS = 80_000_000
 DP_TOUCH_FIXED_PAIRS = 125_000_000
-DP_MIN_PAIRS = 50_000_000
+DP_MIN_PAIRS = 80_000_000  # the CLI's --dp-min-pairs-per-rank default
 DP_MERGES_PER_EPOCH = 7
 DP_ALIGN_MERGES_PER_EPOCH = DP_MERGES_PER_EPOCH  # (round-3 name)
 DP_TOUCH_EVERY_JOBS = 3584

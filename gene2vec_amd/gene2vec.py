@@ -243,18 +243,21 @@ def main(argv=None):
                         default="auto",
                         help="data-parallel replica merge rule: auto = touch every "
                              "--merge-every-jobs jobs from 125 M pairs per rank, touch at 7 "
-                             "merges per epoch from 80 M, align at 7 merges per epoch from 50 M "
-                             "(DESIGN.md 7a/7b); an explicit rule uses --merge-every-jobs")
+                             "merges per epoch from 80 M, align at 7 merges per epoch below "
+                             "(only with a lowered --dp-min-pairs-per-rank; DESIGN.md 7a/7b); "
+                             "an explicit rule uses --merge-every-jobs")
     parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
                         default="auto",
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
                              "collective (gloo) = auto; torch = torch-owned tables merged by "
                              "torch.distributed")
-    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=50_000_000,
+    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=80_000_000,
                         help="under torchrun, shard the pairs only when every rank gets at least "
                              "this many; a smaller corpus trains whole on every rank (no merges, "
-                             "rank 0 writes): merged replicas of smaller shards lag one model on "
-                             "the target function whatever the rule (DESIGN.md 7b)")
+                             "rank 0 writes).  80 M is the smallest shard where a measured merge "
+                             "rule holds the target function within 1 %% of one model (DESIGN.md "
+                             "7b); 50 M .. 80 M (align rule, up to +2 %% there) and anything "
+                             "below (-2.6 %% at best) are explicit opt-ins")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "

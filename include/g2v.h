@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define G2V_ABI_VERSION 4
+#define G2V_ABI_VERSION 5
 
 /* status codes */
 #define G2V_OK 0
@@ -126,18 +126,18 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         every wave trains, no cap [0]
  *   G2V_OPT_TABLE_MEM     context-owned table memory: 0 hipMalloc, 1 fine-grained,
  *                         2 uncached (re-allocates, zero-filled) [0]
- *   G2V_OPT_DEBUG_WRITE   ablation only, breaks training: 1 plain stores instead of
- *                         atomics, 2 no table writes, 3 packed-f16 / 4 f32
- *                         atomics into a scratch table, 5 syn1neg atomics only
- *                         (syn0 never written), 6 stripe copies written but
- *                         never read (readers see main rows only), 7 = 4 with
- *                         main-row-only reads, 8 = the production kernel with
- *                         s_memtime stamps per loop segment (diagnostic build,
- *                         K 5 / D <= 256: g2v_debug_stamps; its run time is
- *                         not a measurement, its segment SHARES are), 9 = the
- *                         production kernel without each row's last atomic
- *                         instruction (a probe of the per-wave instruction
- *                         count; breaks training) [0]
+ *   G2V_OPT_DEBUG_WRITE   measurement builds of the Hogwild kernel, negative 5
+ *                         and vector_size <= 256 only: 2 = no table writes
+ *                         (the write-free gather roof bench.py reports; breaks
+ *                         training), 8 = the production kernel with s_memtime
+ *                         stamps per loop segment (diagnostic build:
+ *                         g2v_debug_stamps; its run time is not a measurement,
+ *                         its segment SHARES are).  The throughput ablations
+ *                         1, 3, 4, 5, 6, 7, 9 (profiles/r0*)
+ *                         exist only in the -DG2V_ABLATIONS build
+ *                         (gene2vec_amd.build.build(ablations=True)); any
+ *                         mode this library does not compile, or a shape it
+ *                         is not compiled for, is G2V_EINVAL [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
  *   G2V_OPT_STRIPE2_ROWS  second stripe tier: rows [STRIPE_ROWS, this) get
  *                         STRIPE2_COPIES copies each (<= STRIPE_ROWS = off);
@@ -172,19 +172,17 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         with G2V_OPT_GRID 1 and 1 wave the production kernel
  *                         runs its chunks in record order, a deterministic
  *                         update order (parity checks) [4]
- *   G2V_OPT_ATOMIC_TAILS  Hogwild kernel at D 193..201 with negative 5 (the
- *                         reference's dim 200): 1 = the K+2 rows' last D-192
- *                         floats go out together in one atomic instruction
- *                         (22 instead of 28 per example), 0 = one tail
- *                         instruction per row [0: one instruction over seven
- *                         rows measured 1.5-4 % slower, DESIGN.md 5d]
- *   G2V_OPT_COPY_DEFER    Hogwild kernel at D <= 256: 1 = the last (up to 7)
- *                         copies of an example's first 3 striped rows stay
- *                         in flight with the main rows
- *                         under the previous example's atomics and are summed
- *                         at first use, 0 = every copy is summed before the
- *                         main rows are requested (same values either way)
- *                         [0: 2-3.5 % slower in its 3-slot form, DESIGN.md 5d]
+ *   G2V_OPT_TAIL_STORE    Hogwild kernel, vector_size <= 256 and negative <= 7
+ *                         (experiment): rows with index >= n
+ *                         (never a striped row) of an example without a
+ *                         repeated target take plain write-through stores of
+ *                         their new value instead of float atomics of the
+ *                         delta -- gensim's own unsynchronised read-modify-
+ *                         write, which loses an update when another wave
+ *                         wrote the row between this wave's read and its
+ *                         store; 0 = off [0]
+ *   (keys 19 and 20, G2V_OPT_ATOMIC_TAILS / G2V_OPT_COPY_DEFER of ABI 4, were
+ *    retired in ABI 5: both measured slower; G2V_EINVAL)
  *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the
  *                         n-th in-call merge of every g2v_train call fails
  *                         before its collective, as a rank that dies between
@@ -208,8 +206,9 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
 #define G2V_OPT_MERGE_BETA_MILLI 16
 #define G2V_OPT_MERGE_GAMMA_MILLI 17
 #define G2V_OPT_DEBUG_FAIL_MERGE 18
-#define G2V_OPT_ATOMIC_TAILS 19
-#define G2V_OPT_COPY_DEFER 20
+#define G2V_OPT_RETIRED_19 19
+#define G2V_OPT_RETIRED_20 20
+#define G2V_OPT_TAIL_STORE 21
 int g2v_set_option(g2v_ctx *ctx, int key, int64_t value);
 /* Current value of an option (G2V_OPT_GRID: the workgroups g2v_set_vocab
  * chose -- by default the staleness budget's, at most one per CU; the

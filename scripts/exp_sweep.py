@@ -39,10 +39,15 @@ def main():
     p.add_argument("--configs", nargs="+", default=["ld=224"])
     p.add_argument("--epochs-eval", action="store_true",
                    help="print the held-in objective after every epoch")
+    p.add_argument("--ablations", action="store_true",
+                   help="load the -DG2V_ABLATIONS build (debug write modes 1, 3-7, 9)")
     a = p.parse_args()
     import torch
 
     from gene2vec_amd import _native as N
+    if a.ablations:
+        from gene2vec_amd import build as B
+        N.use_library(B.build(ablations=True))
     from gene2vec_amd import engine as E
     from gene2vec_amd import synthetic as S
     from oracle import sgns_oracle as O

@@ -53,7 +53,7 @@ def main(out):
         # the kernel build these counters belong to (bench.py refuses any other)
         "kernel_src_sha16": kernel_source_hash(),
         "launch": {k: b["roofline"][k] for k in ("grid_workgroups", "stripes", "stripes_tier2",
-                                                  "atomic_tails", "copy_defer")},
+                                                  "tail_store")},
         "vocab": cfg.get("vocab_requested", cfg["vocab"]), "dim": cfg["dim"], "negative": cfg["negative"],
         "sample": cfg["sample"], "zipf": cfg.get("zipf", 1.0), "kernel": KERNEL,
         "method": "rocprofv3 --pmc, one counter group per run (scripts/profile_round.sh), "

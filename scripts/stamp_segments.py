@@ -40,11 +40,16 @@ def main():
     ap.add_argument("--arms", default="production,stamped,production_again",
                     help="production, stamped (debug write 8), notail (debug write 9: each "
                          "row's last atomic instruction dropped, a throughput probe), copiesN "
-                         "(production with G2V_OPT_STRIPE_COPIES N), tailsN (production with "
-                         "G2V_OPT_ATOMIC_TAILS N), deferN (production with G2V_OPT_COPY_DEFER "
-                         "N), stamped_deferN, any suffix _again")
+                         "(production with G2V_OPT_STRIPE_COPIES N), tailN (production with "
+                         "G2V_OPT_TAIL_STORE N), stamped_tailN, any suffix _again; notail "
+                         "needs the ablation build (--ablations)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ablations", action="store_true",
+                    help="load the -DG2V_ABLATIONS build (debug write modes 1, 3-7, 9)")
     a = ap.parse_args()
+    if a.ablations:
+        from gene2vec_amd import build as B
+        N.use_library(B.build(ablations=True))
     D, K = 200, 5
     pairs = S.zipf_gene_pairs(a.pairs, a.vocab, 1.0, seed=20250114)
     flat = pairs.reshape(-1)
@@ -68,15 +73,13 @@ def main():
     out = {"config": {"pairs": a.pairs, "vocab": a.vocab, "sample": a.sample, "D": D, "K": K},
            "arms": {}}
     buf = np.zeros(16, np.uint64)
-    tails0 = eng.get_option(N.OPT_ATOMIC_TAILS)  # the library's defaults = "production"
-    defer0 = eng.get_option(N.OPT_COPY_DEFER)
     for arm in a.arms.split(","):
         base = arm.replace("_again", "")
         dbg = 8 if base.startswith("stamped") else {"notail": 9}.get(base, 0)
         eng.set_option(N.OPT_DEBUG_WRITE, dbg)
         eng.set_option(N.OPT_STRIPE_COPIES, int(base[6:]) if base.startswith("copies") else 0)
-        eng.set_option(N.OPT_ATOMIC_TAILS, int(base[5:]) if base.startswith("tails") else tails0)
-        eng.set_option(N.OPT_COPY_DEFER, int(base[-1]) if "defer" in base else defer0)
+        tail = base.split("tail")[-1] if "tail" in base and base != "notail" else "0"
+        eng.set_option(N.OPT_TAIL_STORE, int(tail))
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)  # warm (and |syn1| grows)
         eng.read_stats()
         eng._lib.g2v_debug_stamps(eng._h, N.ptr(buf), 16)

@@ -23,7 +23,7 @@ def test_cli_defaults_match_the_c3_gate():
     jobs from 125 M pairs per rank and sharding from 50 M; the reference's own settings
     (src/gene2vec.py:57-63) stay the CLI's"""
     a = _parsed(["d", "o", "txt"])
-    assert a["merge_every_jobs"] == 3584 and a["dp_min_pairs_per_rank"] == 50_000_000
+    assert a["merge_every_jobs"] == 3584 and a["dp_min_pairs_per_rank"] == 80_000_000
     assert a["merge_rule"] == "auto"
     assert (a["dim"], a["negative"], a["window"], a["sample"], a["iters"], a["workers"]) == \
         (200, 5, 1, 1e-3, 10, 32)

@@ -106,37 +106,81 @@ def test_one_wave_chunk_boundaries_and_short_tail():
         assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (n, _rel(g0, r0), _rel(g1, r1))
 
 
-@pytest.mark.parametrize("stripes", ["default", "two_tier"])
-def test_kernel_variants_same_values(stripes):
-    """the instances G2V_OPT_ATOMIC_TAILS / G2V_OPT_COPY_DEFER choose between
-     change only the instruction schedule: on one wave each
-    matches the restatement and they agree with each other to rounding"""
-    V, D, K, n, alpha = 40, 200, 5, 3000, 0.025
-    rng = np.random.RandomState(7)
+def _no_consecutive_share(V, K, n, seed):
+    """Zipf examples in which no row of either table recurs in the NEXT
+    example (the one whose loads overtake this example's writes)"""
+    rng = np.random.RandomState(seed)
+    p = 1.0 / np.arange(1, V + 1)
+    p /= p.sum()
+    c = np.empty(n, np.int32)
+    i = np.empty(n, np.int32)
+    negs = np.empty((n, K), np.int32)
+    prev1, prev0 = set(), set()
+    for e in range(n):
+        while True:
+            ce, ie = rng.choice(V, 2, p=p)
+            ne = rng.choice(V, K, p=p)
+            s1 = {int(ce), *map(int, ne)}
+            if not (s1 & prev1) and int(ie) not in prev0:
+                break
+        ne[ne == ce] = -1
+        c[e], i[e], negs[e] = ce, ie, ne
+        prev1, prev0 = s1, {int(ie)}
+    return c, i, negs
+
+
+@pytest.mark.parametrize("tail", [100, 1])
+def test_one_wave_tail_stores_match_restatement(tail):
+    """G2V_OPT_TAIL_STORE: on one wave, with no row shared by
+    consecutive examples, a cold row's plain store of (row as read + delta)
+    leaves the same value as the atomic (row + delta): the kernel still
+    matches orc_atomic_one_wave at 1e-5, repeated targets (atomics) included;
+    tail 1 = every unstriped row stored"""
+    V, D, K, n, alpha = 2000, 200, 5, 1500, 0.025
+    rng = np.random.RandomState(3)
     syn0 = ((rng.rand(V, D) - 0.5) / D).astype(np.float32)
     syn1 = ((rng.rand(V, D) - 0.5) / D * 0.1).astype(np.float32)
     lockf = np.ones(V, np.float32)
-    c, i, negs = _examples(V, K, n, seed=11)
-    out = {}
-    for tails in (0, 1):
-        for defer in (0, 1):
-            e = E.SGNSEngine(V, D, K)
-            e.set_weights(syn0, syn1)
-            e.set_option(N.OPT_GRID, 1)
-            e.set_option(N.OPT_ACTIVE_WAVES, 1)
-            e.set_option(N.OPT_ATOMIC_TAILS, tails)
-            e.set_option(N.OPT_COPY_DEFER, defer)
-            for k, v in STRIPES[stripes].items():
-                e.set_option(k, v)
-            e.step_explicit(c, i, negs, alpha, mode=N.MODE_HOGWILD)
-            out[tails, defer] = e.get_weights()
-            st = e.read_stats()
-            e.close()
+    c, i, negs = _no_consecutive_share(V, K, n, seed=tail)
+    negs[5::97, 1] = negs[5::97, 0]  # some repeated targets: those examples keep atomics
+    e = E.SGNSEngine(V, D, K)
+    e.set_weights(syn0, syn1)
+    e.set_option(N.OPT_GRID, 1)
+    e.set_option(N.OPT_ACTIVE_WAVES, 1)
+    for k, v in STRIPES["two_tier"].items():
+        e.set_option(k, v)
+    e.set_option(N.OPT_TAIL_STORE, tail)
+    assert e.get_option(N.OPT_TAIL_STORE) == tail
+    e.step_explicit(c, i, negs, alpha, mode=N.MODE_HOGWILD)
+    g0, g1 = e.get_weights()
+    st = e.read_stats()
+    e.close()
     r0, r1 = syn0.copy(), syn1.copy()
     CO.atomic_one_wave(r0, r1, lockf, c, i, negs, alpha, st["stripe_rows"], st["stripe_copies"],
                        st["stripe2_rows"], st["stripe2_copies"])
-    base0, base1 = out[0, 0]  # the defaults
-    for key, (g0, g1) in out.items():
-        assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (key, _rel(g0, r0), _rel(g1, r1))
-        assert _rel(g0, base0) < 1e-6 and _rel(g1, base1) < 1e-6, (key, _rel(g0, base0),
-                                                                   _rel(g1, base1))
+    assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (_rel(g0, r0), _rel(g1, r1))
+    assert np.abs(g1 - syn1).max() > 0
+
+
+def test_retired_and_unsupported_options_refused():
+    """ABI 5: the measured-slower kernel variants are gone (keys 19 / 20), and
+    a debug build or tail stores on a shape the library does not compile them
+    for is G2V_EINVAL, not a silent production run"""
+    e = E.SGNSEngine(100, 512, 15)
+    try:
+        for key, val in ((19, 1), (20, 1), (N.OPT_DEBUG_WRITE, 8), (N.OPT_DEBUG_WRITE, 2),
+                         (N.OPT_DEBUG_WRITE, 1), (N.OPT_TAIL_STORE, 50)):
+            with pytest.raises(N.G2VError):
+                e.set_option(key, val)
+    finally:
+        e.close()
+    e = E.SGNSEngine(100, 200, 5)
+    try:
+        e.set_option(N.OPT_DEBUG_WRITE, 8)
+        e.set_option(N.OPT_DEBUG_WRITE, 2)
+        e.set_option(N.OPT_DEBUG_WRITE, 0)
+        for bad in (1, 3, 4, 5, 6, 7, 9):  # ablations: -DG2V_ABLATIONS build only
+            with pytest.raises(N.G2VError):
+                e.set_option(N.OPT_DEBUG_WRITE, bad)
+    finally:
+        e.close()

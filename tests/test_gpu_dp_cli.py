@@ -150,7 +150,7 @@ def test_cli_data_parallel_ragged_corpus_falls_back(tmp_path):
 
 
 def test_cli_small_corpus_trains_whole_on_every_rank(tmp_path):
-    """below --dp-min-pairs-per-rank (default 50 M) the CLI does not shard:
+    """below --dp-min-pairs-per-rank (default 80 M) the CLI does not shard:
     merged replicas of small shards learn far less than one model (DESIGN.md
     7b: 8 x 1.25 M pairs, 10 iterations, held-in objective +36 %), so every
     rank trains the whole corpus and rank 0's outputs match a single-process

@@ -14,7 +14,7 @@ the one model's (measured +0.18 % / +0.09 %) -- the merge converges.
 This is NOT the north star's quality claim: at 12.5 M pairs per replica the
 manuscript target function of merged replicas lags one model by 2.6-8 % on a
 corpus with planted modules whatever the rule and cadence,
-which is why the CLI does not shard below --dp-min-pairs-per-rank = 50 M.  The
+which is why the CLI does not shard below --dp-min-pairs-per-rank = 80 M.  The
 target function within 1 % is gated at C3's full size, 8 x 125 M pairs, and
 at 8 x 50 M pairs with the align plan by tests/test_gpu_c3_quality.py."""
 import zlib

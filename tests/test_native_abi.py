@@ -27,7 +27,7 @@ def test_library_loads_and_exports_header():
         assert hasattr(L, s), s
         assert s in N.SIGNATURES, f"{s} missing from the ctypes signature table"
     assert set(N.SIGNATURES) == set(syms)
-    assert L.g2v_abi_version() == N.ABI_VERSION == 4
+    assert L.g2v_abi_version() == N.ABI_VERSION == 5
 
 
 def test_error_path_without_gpu_is_loud():
