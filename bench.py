@@ -75,10 +75,12 @@ def parse():
     p.add_argument("--negative", type=int, default=5)
     p.add_argument("--sample", type=float, default=1e-3)
     p.add_argument("--zipf", type=float, default=1.0)
-    p.add_argument("--avg-every-jobs", type=int, default=3584,
-                   help="replica merge cadence in jobs per rank (N>1; the CLI's default)")
-    p.add_argument("--merge", choices=("touch", "mean"), default="touch",
-                   help="replica merge rule (gene2vec_amd.distributed)")
+    p.add_argument("--avg-every-jobs", type=int, default=0,
+                   help="replica merge cadence in jobs per rank (N>1; 0 = the CLI's plan, "
+                        "distributed.dp_merge_plan: once per epoch up to 4 GPUs, every 3,584 "
+                        "jobs beyond)")
+    p.add_argument("--merge", choices=("auto", "touch", "mean", "align"), default="auto",
+                   help="replica merge rule (auto = the CLI's plan, gene2vec_amd.distributed)")
     p.add_argument("--grid", type=int, default=0, help="SGNS workgroups (0 = library default)")
     p.add_argument("--stripe", default="", help="hot-row stripes ROWSxCOPIES (default: library's)")
     p.add_argument("--stripe2", default="",
@@ -289,7 +291,10 @@ def main():
     alphas = E.job_alphas(js, n_pairs)
     rs = np.random.RandomState(Dd.rank_seed(1, rank))  # gensim model.random(seed=1) per rank
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
-    avg_every = max(1, a.avg_every_jobs) if use_dist else n_jobs
+    merge_rule, avg_every = Dd.dp_merge_plan(n_pairs, a.avg_every_jobs or None, a.merge,
+                                             jobs_per_rank=n_jobs, world=world)
+    if not use_dist:
+        avg_every = n_jobs
     merge_backend = "torch"
     merge_note = None
     if use_dist and ((a.backend == "nccl" and a.merge_transport == "auto")
@@ -311,7 +316,7 @@ def main():
         # gloo rehearsal: libg2v's merge, its all-reduce carried through the host
         eng.comm_init_host(Dd.host_collective(), world, rank)
         merge_backend = "libg2v-host"
-    trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=a.merge,
+    trainer = Dd.ReplicaTrainer(eng, (tables,), avg_every, N.MODE_HOGWILD, merge=merge_rule,
                                 backend="torch" if merge_backend == "torch" else "libg2v")
     torch.cuda.synchronize(dev)
 
@@ -530,7 +535,7 @@ def main():
                              f"{n_pairs} pairs, dim {D}, neg {K}, window 1, sample {a.sample:g}, "
                              "1 epoch per step") if world == 1 else
                             (f"C3: synthetic Zipf gene pairs, V={V0}, {n_pairs} pairs per GPU x "
-                             f"{world}, dim {D}, neg {K}, replica merge ({a.merge}) every "
+                             f"{world}, dim {D}, neg {K}, replica merge ({merge_rule}) every "
                              f"{avg_every} jobs: "
                              + (("libg2v g2v_average (RCCL over xGMI)" if a.backend == "nccl"
                                  else "libg2v RCCL merge path through G2V_RCCL_LIB (rehearsal, "
@@ -542,7 +547,7 @@ def main():
                                 "torch.distributed merge (libg2v communicator unavailable)")),
                 "vocab": V, "vocab_requested": V0, "zipf": a.zipf, "pairs_per_gpu": n_pairs,
                 "dim": D, "negative": K, "sample": a.sample, "window": 1,
-                "parallelism": f"dp{world}" + (f" + {merge_backend} {a.merge} merge"
+                "parallelism": f"dp{world}" + (f" + {merge_backend} {merge_rule} merge"
                                                if world > 1 else "")},
             # per-GPU rate beside the shard it trained: N = 1 trains the C2
             # 100 M pairs without merges, N > 1 a 125 M-pair shard per rank
@@ -551,7 +556,7 @@ def main():
             "examples_per_s": round(total_examples / elapsed, 1),
             "effective_examples": total_examples,
             "roofline": roofline, "cpu_baseline": cpu, "quality": quality,
-            "merge": ({"backend": merge_backend, "rule": a.merge, "every_jobs": avg_every,
+            "merge": ({"backend": merge_backend, "rule": merge_rule, "every_jobs": avg_every,
                        "merges": trainer.averages, "note": merge_note} if world > 1 else None),
             "gpu_event_ms": round(gpu_ms, 3), "wall_s": round(wall, 4),
             "step_ms_rank0": step_ms, "step_ms_median_rank0": float(np.median(step_ms)),

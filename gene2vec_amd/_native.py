@@ -76,7 +76,8 @@ class Stats(C.Structure):
                 ("training_loss", C.c_double), ("sgns_grid", C.c_int64),
                 ("stripe_rows", C.c_int64), ("stripe_copies", C.c_int64),
                 ("stripe2_rows", C.c_int64), ("stripe2_copies", C.c_int64),
-                ("sgns_waves", C.c_int64)]
+                ("sgns_waves", C.c_int64), ("tail_row_syn0", C.c_int64),
+                ("tail_row_syn1neg", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

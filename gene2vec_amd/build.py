@@ -54,7 +54,7 @@ def hipcc() -> str:
 # the throughput-ablation build (G2V_OPT_DEBUG_WRITE 1, 3-7, 9):
 # the same sources with -DG2V_ABLATIONS, a library of its own that is never
 # shipped or loaded by the product (scripts load it with _native.use_library)
-ABLATIONS_LIB = os.path.join(HERE, "build", "libg2v_ablations.so")
+ABLATIONS_LIB = os.path.join(HERE, "libg2v_ablations.so")
 
 
 def _stale(lib=LIB) -> bool:

@@ -147,7 +147,10 @@ struct g2v_ctx {
   float* stripe2 = nullptr;
   int64_t stripe2_cap = 0;
   int atomic_overlap = 1;
-  int tail_store = 0;  // G2V_OPT_TAIL_STORE: first row of the plain-store tail, 0 = off
+  int tail_store = -1;  // G2V_OPT_TAIL_STORE: -1 auto (collision budget), 0 off, n rows >= n
+  // per row (index order) from set_vocab: u(r) = K p_neg(r) + p_tok(r) (syn1neg
+  // updates per example) and p_tok(r) (syn0), the tail stores' collision budget
+  std::vector<double> u_row, ptok_row;
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int64_t debug_fail_merge = 0;  // G2V_OPT_DEBUG_FAIL_MERGE: fault injection
@@ -242,6 +245,7 @@ struct g2v_ctx {
   int active_waves = 4;  // G2V_OPT_ACTIVE_WAVES
   int last_grid = 0, last_stripe_rows = 0, last_stripe_copies = 1, last_stripe2_rows = 0,
       last_stripe2_copies = 1;  // layout of the last Hogwild launch (g2v_stats)
+  int last_tail0 = -1, last_tail1 = -1;  // its tail-store rows (-1: none)
   int64_t jobs = 0, launches = 0;
 
   // timing
@@ -280,6 +284,25 @@ constexpr double kStaleBudget = 125.0;
 // reaches 100 (round 3 evaluated it once per g2v_train call, from a host
 // read-back; a whole data-parallel epoch in one call was never re-capped).
 constexpr double kSyn0Budget = 100.0;
+
+// Cold-row plain stores (G2V_OPT_TAIL_STORE auto; k_sgns_atomic, DESIGN.md
+// 5e).  A row whose update is a plain store of (row as read + delta) loses
+// another wave's update when that wave writes it inside this wave's read-to-
+// store window; waves x (the row's updates per example) estimates how many
+// other in-flight examples hold it.  Auto: syn1neg rows from the first r with
+// waves x u(r) <= this budget take stores (never a striped row); syn0 rows
+// keep atomics.  C2 (1,024 waves): syn1neg from row ~7,700, 25 % of the
+// syn1neg updates; corpora of <= ~5,000 genes have no syn1neg row this cold
+// at their default grid.  Measured (profiles/r05): both tables
+// from row 8,192 at C2 = +10.7 % pairs/s, 9.4 % of the stores lost an update
+// (lost-update probe), the C2-vocabulary end-to-end gate at loss +0.38 %,
+// objective +0.23 %, target function -0.43 % (atomics: +0.07 / -0.05 /
+// -0.09 %); from 4,096 +12.4 %, 12 % lost, +0.58 / +0.42 / -0.63 %; from
+// 2,048 the objective (+0.56 %) fails its 0.5 % bar.  syn0 rows by the same
+// budget (p_tok(r), from row ~850 at C2, ~1,100 at 3,000-5,000 genes) took
+// the dense 5,000-gene gate's target function from -0.46 to -0.84 % (1 %
+// bar): syn0 holds the exported vectors, so it stays exact.
+constexpr double kTailCollision = 0.15;
 
 // Copies per striped hot row when G2V_OPT_STRIPE_COPIES is not set.  Every
 // read of a striped row sums its copies (one more load batch on the example's
@@ -364,9 +387,20 @@ const Rccl& rccl() {
     void* h = nullptr;
     // G2V_RCCL_LIB names another library with RCCL's entry points and nothing
     // else is tried (the test suite's stand-in, tests/rccl_standin/: two
-    // ranks on ONE GPU, which real RCCL refuses as "Duplicate GPU")
+    // ranks on ONE GPU, which real RCCL refuses as "Duplicate GPU").  It takes
+    // effect only with the second opt-in G2V_ALLOW_RCCL_STANDIN=1, and says so
+    // on stderr, so a stray variable cannot silently route real multi-GPU
+    // merges through another library
     const char* over = getenv("G2V_RCCL_LIB");
+    const char* allow = getenv("G2V_ALLOW_RCCL_STANDIN");
+    if (over && *over && !(allow && std::string(allow) == "1")) {
+      fprintf(stderr, "libg2v: ignoring G2V_RCCL_LIB=%s (set G2V_ALLOW_RCCL_STANDIN=1 to load it "
+                      "instead of RCCL)\n", over);
+      over = nullptr;
+    }
     if (over && *over) {
+      fprintf(stderr, "libg2v: G2V_RCCL_LIB=%s replaces RCCL for every merge of this process\n",
+              over);
       h = dlopen(over, RTLD_NOW | RTLD_LOCAL);
       r.library = over;
     } else {
@@ -675,7 +709,7 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       // build (-DG2V_ABLATIONS).  Refused otherwise instead of silently
       // running the production kernel.
 #ifdef G2V_ABLATIONS
-      const bool known = value >= 0 && value <= 9;
+      const bool known = value >= 0 && value <= 10;
 #else
       const bool known = value == 0 || value == 2 || value == 8;
 #endif
@@ -723,9 +757,9 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       return fail(G2V_EINVAL, "option %d was retired in ABI 5 (measured slower, DESIGN.md 5d)",
                   key);
     case G2V_OPT_TAIL_STORE:
-      REQUIRE(value >= 0 && value <= c->V, G2V_EINVAL, "tail store row %lld out of [0, V]",
+      REQUIRE(value >= -1 && value <= c->V, G2V_EINVAL, "tail store row %lld out of [-1, V]",
               (long long)value);
-      REQUIRE(value == 0 || (c->nv == 1 && c->K + 1 <= 8), G2V_EINVAL,
+      REQUIRE(value <= 0 || (c->nv == 1 && c->K + 1 <= 8), G2V_EINVAL,
               "tail stores need vector_size <= 256 and negative <= 7");
       c->tail_store = (int)value;
       return G2V_OK;
@@ -805,6 +839,12 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
     }
     c->u_max = um;
     c->p_tok_max = pm;
+    c->u_row.resize((size_t)c->V);
+    c->ptok_row.resize((size_t)c->V);
+    for (int32_t i = 0; i < c->V; ++i) {
+      c->u_row[i] = c->K * pn[i] / zn + pt[i] / zt;
+      c->ptok_row[i] = pt[i] / zt;
+    }
     if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
   }
   HIPCHK(hipMemcpyAsync(c->d_counts, counts, sizeof(int64_t) * c->V, hipMemcpyHostToDevice,
@@ -1157,9 +1197,26 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   }
   s.stripe2 = c->stripe2;
   // cold-row plain stores (G2V_OPT_TAIL_STORE), never on a striped row
-  s.tail_row = (c->tail_store > 0 && c->debug_write == 0)
-                   ? std::max(c->tail_store, std::max(s.stripe_rows, s.stripe2_rows))
-                   : 0x7fffffff;
+  s.tail_row0 = s.tail_row1 = 0x7fffffff;
+  if (atomic_kernel && (c->debug_write == 0 || c->debug_write == 10) && c->nv == 1 &&
+      c->K + 1 <= 8 && c->tail_store != 0) {
+    int t0 = c->tail_store, t1 = c->tail_store;
+    if (c->tail_store < 0) {
+      // auto: the collision budget over the waves this launch may run
+      // (u(r), p_tok(r) are non-increasing in r: counts are sorted)
+      const double waves = (double)launch_grid(c) * c->active_waves;
+      auto first_under = [&](const std::vector<double>& rate) {
+        return (int)(std::partition_point(rate.begin(), rate.end(),
+                                          [&](double x) { return waves * x > kTailCollision; }) -
+                     rate.begin());
+      };
+      t1 = c->u_row.empty() ? c->V : first_under(c->u_row);
+      t0 = c->V;  // syn0 (the exported vectors) keeps atomics: see kTailCollision
+    }
+    const int floor_row = std::max(s.stripe_rows, s.stripe2_rows);
+    if (t0 < c->V) s.tail_row0 = std::max(t0, floor_row);
+    if (t1 < c->V) s.tail_row1 = std::max(t1, floor_row);
+  }
   if (c->debug_write == 3 || c->debug_write == 4 || c->debug_write == 7) {
     const int64_t rows = (int64_t)c->V + (int64_t)(s.stripe_copies - 1) * s.stripe_rows;
     const int64_t words = rows * c->ld * (c->debug_write == 3 ? 1 : 2);
@@ -1167,7 +1224,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     HIPCHK(hipMemsetAsync(c->dbg16, 0, sizeof(uint32_t) * c->dbg16_cap, c->stream));
   }
   s.dbg16 = c->dbg16;
-  if (c->debug_write == 8 && !c->d_stamps) {
+  if ((c->debug_write == 8 || c->debug_write == 10) && !c->d_stamps) {
     if ((rc = dev_alloc(&c->d_stamps, kStampWords))) return rc;
     HIPCHK(hipMemsetAsync(c->d_stamps, 0, kStampWords * sizeof(unsigned long long), c->stream));
   }
@@ -1207,6 +1264,8 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     c->last_stripe_copies = s.stripe_copies;
     c->last_stripe2_rows = s.stripe2_rows;
     c->last_stripe2_copies = s.stripe2_copies;
+    c->last_tail0 = s.tail_row0 < c->V ? s.tail_row0 : -1;
+    c->last_tail1 = s.tail_row1 < c->V ? s.tail_row1 : -1;
   }
   c->launches++;
   return G2V_OK;
@@ -1587,6 +1646,8 @@ int g2v_read_stats(g2v_ctx* c, g2v_stats* out) {
   int waves = 0;
   if (c->last_grid > 0) HIPCHK(hipMemcpy(&waves, c->d_waves, sizeof waves, hipMemcpyDeviceToHost));
   out->sgns_waves = waves;
+  out->tail_row_syn0 = c->last_tail0;
+  out->tail_row_syn1neg = c->last_tail1;
   for (auto& p : c->t_sgns) {
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, p.first, p.second));

@@ -119,8 +119,8 @@ struct SgnsArgs {
   float cap_coef;           // p_tok_max x (K+1) x the launch's largest alpha
   float cap_budget;
   int* waves_out;           // the waves that trained (block 0 writes it)
-  int tail_row;             // G2V_OPT_TAIL_STORE: rows >= this take plain stores
-                            // (k_sgns_atomic, repeat-free examples; >= V: none)
+  int tail_row0;            // G2V_OPT_TAIL_STORE: syn0 rows >= this and syn1neg
+  int tail_row1;            // rows >= tail_row1 take plain stores (k_sgns_atomic)
   // compute_loss ([ext] fast_sentence_sg_neg's LOG_TABLE tally)
   int compute_loss;
   const float* log_table;   // [1000] (float)log(EXP_TABLE[i])

@@ -32,7 +32,7 @@ namespace g2v {
 // write-free gather roof bench.py measures) and 8 (s_memtime stamps,
 // scripts/stamp_segments.py).  The throughput ablations (WR 1, 3, 4, 5, 9 and
 // G2V_OPT_DEBUG_WRITE 6 / 7) exist only in the -DG2V_ABLATIONS build
-// (gene2vec_amd.build.build(ablations=True) -> build/libg2v_ablations.so).
+// (gene2vec_amd.build.build(ablations=True) -> gene2vec_amd/libg2v_ablations.so).
 constexpr int kStripeBatch = 7;
 constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
 
@@ -221,7 +221,8 @@ __device__ __forceinline__ void add_copies(ExRegs<K, NV>& x) {
 // (tables never written), 5 production atomics on syn1neg only, syn0 never
 // written (the ceiling of any syn0-side combining), 9 production without each
 // row's last atomic instruction (elements 192..255 at D <= 256: a throughput
-// probe of the per-wave instruction count; breaks training)
+// probe of the per-wave instruction count; breaks training), 10 production
+// with the lost-update probe on every cold-row store (lost_probe)
 //
 // One row's delta coef * src[0, D) as a FIXED 4 * NV wave-instructions: the
 // buffer resource spans the row's D floats, so lanes past D (and every lane of
@@ -251,22 +252,23 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 #endif
     const int off = (64 * i + lane) * 4;
     const float v = coef * src[i];
-    if (WR == 0 || WR == 4 || WR == 5 || WR == 8 || WR == 9)
+    if (WR == 0 || WR == 4 || WR == 5 || WR == 8 || WR == 9 || WR == 10)
       __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(v, r, off, 0, 0);
     else if (WR == 1)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off, 0, 0);
   }
 }
 
-// G2V_OPT_TAIL_STORE (experiment; off by default): a cold row
-// (index >= a.tail_row, never striped) of a repeat-free example is written
-// with plain stores of its new value, the element-order row val[0, 4 NV),
-// instead of float atomics of the delta: the same 4 NV wave-instructions of
-// 256 contiguous bytes (so the loop head's vmcnt count is the same on both
-// paths), write-through (sc1: the line leaves the writer's L2, so a later read
-// on that XCD fetches the memory side's copy).  gensim's own Hogwild
-// read-modify-write, with the lost updates that implies when another wave
-// wrote the row between this wave's read and its store.
+// G2V_OPT_TAIL_STORE: a cold row (syn0 index >= a.tail_row0,
+// syn1neg index >= a.tail_row1, never a striped row; syn1neg rows only in a
+// repeat-free example) is written with plain stores of its new value, the
+// element-order row val[0, 4 NV), instead of float atomics of the delta: the
+// same 4 NV wave-instructions of 256 contiguous bytes, write-through (sc1: the
+// line leaves the writer's L2, so a later read on that XCD fetches the memory
+// side's copy).  gensim's own Hogwild read-modify-write, with the lost updates
+// that implies when another wave wrote the row between this wave's read and
+// its store -- which is why only rows that other in-flight waves rarely touch
+// take it (run_sgns's collision budget).
 template <int NV>
 __device__ __forceinline__ void store_row(float* row, bool live, int D, const float (&val)[4 * NV],
                                           int lane) {
@@ -276,6 +278,25 @@ __device__ __forceinline__ void store_row(float* row, bool live, int D, const fl
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val[i]), r, (64 * i + lane) * 4, 0,
                                           Pol<kPolWt>::st);
 }
+
+#ifdef G2V_ABLATIONS
+// WR 10 (ablation build): before a cold row's store, re-read its first 64
+// floats write-through-fresh (sc1: past this CU's L1) and compare them with
+// the values this wave read for its update (old = element `lane`); a
+// difference means another wave wrote the row inside this wave's read-to-
+// store window, and the store about to land overwrites that update -- one
+// lost update.  stamps[14] += stores probed, stamps[15] += rows changed.
+__device__ __forceinline__ void lost_probe(float* row, float old, unsigned long long* stamps,
+                                           int lane) {
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row, true, 64);
+  const float now = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, lane * 4, 0, 16));
+  const bool changed = __builtin_amdgcn_ballot_w64(now != old) != 0;
+  if (lane == 0) {
+    atomicAdd(stamps + 14, 1ull);
+    if (changed) atomicAdd(stamps + 15, 1ull);
+  }
+}
+#endif
 
 // LOSS ([ext] compute_loss): each wave keeps a float32 partial of the
 // -log(sigmoid(+-f)) LOG_TABLE terms over its chunk and adds it to a double
@@ -335,12 +356,15 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
   constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
-  constexpr bool TS = WR == 0 && tail_ok<K, NV>();  // tail stores compiled in
+  // tail stores compiled in (WR 10, ablation build: the same, with the
+  // lost-update probe)
+  constexpr bool TS = (WR == 0 || WR == 10) && tail_ok<K, NV>();
   __shared__ float s_lut[kExpTableSize];
   __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
   __shared__ float s_wk[W][256 * NV];
   __shared__ float s_tl[W][TS ? NT * 256 : 1];  // tail rows' new values (TS)
+  __shared__ float s_to[W][WR == 10 ? NT * 64 : 1];  // WR 10: their old first 64 floats
   __shared__ int32_t s_rec[W][kChunk * RS];  // the wave's chunk of records
   __shared__ float s_lf[W][kChunk];          // lockf[input] per record of the chunk
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
@@ -386,7 +410,8 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   const int rowb = (int)a.ld * 4;
   // first cold row taking plain stores (V or more: none; run_sgns keeps it
   // past both stripe tiers)
-  const int tail_row = TS ? a.tail_row : 0x7fffffff;
+  const int tail0 = TS ? a.tail_row0 : 0x7fffffff;
+  const int tail1 = TS ? a.tail_row1 : 0x7fffffff;
   float* s1 = s_l1[wid];
   float* sw = s_wk[wid];
   float* stl = s_tl[wid];
@@ -506,8 +531,10 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
             work[v].z = __fmaf_rn(gg, x.rw[d][v].z, work[v].z);
             work[v].w = __fmaf_rn(gg, x.rw[d][v].w, work[v].w);
           }
-          if (TS && x.tg[d] >= tail_row) {
+          if (TS && x.tg[d] >= tail1) {
             // the cold row's new value, staged in element order for store_row
+            if (WR == 10 && lane < 16)
+              *reinterpret_cast<float4*>(s_to[wid] + d * 64 + lane * 4) = x.rw[d][0];
             float4 nw;
             nw.x = __fmaf_rn(gg, x.l1[0].x, x.rw[d][0].x);
             nw.y = __fmaf_rn(gg, x.l1[0].y, x.rw[d][0].y);
@@ -662,24 +689,30 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         float* row = upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb);
-        const bool st = uniform_b(TS && !rep && tg[d] >= tail_row);
+        const bool st = uniform_b(TS && !rep && tg[d] >= tail1);
         emit_row<NV, WR>(row, live[d] && !st, D, v1, g[d], lane);
         if (st) {
           float val[4 * NV];
 #pragma unroll
           for (int i = 0; i < 4 * NV; ++i) val[i] = stl[d * 256 + 64 * i + lane];
+#ifdef G2V_ABLATIONS
+          if (WR == 10 && live[d]) lost_probe(row, s_to[wid][d * 64 + lane], a.stamps, lane);
+#endif
           store_row<NV>(row, live[d], D, val, lane);
         }
         if (WR == 8 && d == 3) sub[2] += stamp_time() - ts;  // 16 atomics issued
       }
       {
         float* row = upd_row<WR>(a, 0, input, cbase + NT, rowb);
-        const bool st = uniform_b(TS && input >= tail_row);
+        const bool st = uniform_b(TS && input >= tail0);
         emit_row<NV, WR>(row, any && !st && WR != 5, D, vw, lf, lane);
         if (st) {
           float val[4 * NV];
 #pragma unroll
           for (int i = 0; i < 4 * NV; ++i) val[i] = __fmaf_rn(lf, vw[i], v1[i]);
+#ifdef G2V_ABLATIONS
+          if (WR == 10 && any) lost_probe(row, v1[0], a.stamps, lane);
+#endif
           store_row<NV>(row, any, D, val, lane);
         }
       }
@@ -745,6 +778,10 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
   if (nv == 1 && a.debug_write == 9) {
     hipLaunchKernelGGL((k_sgns_atomic<5, 1, 9>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+  if (nv == 1 && a.debug_write == 10) {
+    hipLaunchKernelGGL((k_sgns_atomic<5, 1, 10>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
     return hipGetLastError();
   }
 #endif

@@ -344,26 +344,38 @@ DP_MIN_PAIRS = 80_000_000  # the CLI's --dp-min-pairs-per-rank default
 DP_MERGES_PER_EPOCH = 7
 DP_ALIGN_MERGES_PER_EPOCH = DP_MERGES_PER_EPOCH  # (round-3 name)
 DP_TOUCH_EVERY_JOBS = 3584
+# At 2 and 4 ranks (round 5; 125 M pairs per rank, corpora A /
+# B) the merged replicas score ABOVE one model on the target function at every
+# cadence, and least so when they merge once per epoch: touch every 3,584 jobs
+# +1.8 / +3.0 % (2 ranks), +2.2 / +2.1 % (4); once per epoch +1.0 / +2.4..2.6 %
+# (2), +0.3 / +1.3 % (4); the mean rule the same within 0.5 %; held-in,
+# held-out and GGIPNN AUC within 0.4 % everywhere.  So up to this many ranks
+# the plan merges once per epoch (the epoch call's last window).
+DP_EPOCH_MERGE_MAX_WORLD = 4
 
 
-def dp_merge_plan(pairs_per_rank, merge_every_jobs=DP_TOUCH_EVERY_JOBS, rule="auto",
-                  jobs_per_rank=None):
-    """(rule, merge_every_jobs) for a data-parallel run.  rule "auto": touch at
-    merge_every_jobs from DP_TOUCH_FIXED_PAIRS pairs per rank; touch at
-    DP_MERGES_PER_EPOCH merges per epoch (or merge_every_jobs, if more often)
-    from DP_TOUCH_MIN_PAIRS; align at DP_MERGES_PER_EPOCH merges per epoch
-    below (jobs_per_rank: gensim jobs of one rank's epoch; by default a pairs
-    corpus's, 5,000 pairs per 10,000-word job).  An explicit rule keeps
-    merge_every_jobs."""
-    if rule != "auto":
-        return rule, int(merge_every_jobs)
-    if pairs_per_rank >= DP_TOUCH_FIXED_PAIRS:
-        return "touch", int(merge_every_jobs)
+def dp_merge_plan(pairs_per_rank, merge_every_jobs=None, rule="auto", jobs_per_rank=None,
+                  world=8):
+    """(rule, merge_every_jobs) for a data-parallel run of `world` ranks.
+    rule "auto": up to DP_EPOCH_MERGE_MAX_WORLD ranks, touch once per epoch;
+    beyond, touch every merge_every_jobs (default DP_TOUCH_EVERY_JOBS) from
+    DP_TOUCH_FIXED_PAIRS pairs per rank, touch at DP_MERGES_PER_EPOCH merges
+    per epoch (or merge_every_jobs, if more often) from DP_TOUCH_MIN_PAIRS, and
+    align at DP_MERGES_PER_EPOCH merges per epoch below (jobs_per_rank: gensim
+    jobs of one rank's epoch; by default a pairs corpus's, 5,000 pairs per
+    10,000-word job).  An explicit rule or merge_every_jobs is kept."""
     if jobs_per_rank is None:
         jobs_per_rank = -(-int(pairs_per_rank) // 5000)
+    if rule != "auto":
+        return rule, int(merge_every_jobs or DP_TOUCH_EVERY_JOBS)
+    if world <= DP_EPOCH_MERGE_MAX_WORLD:
+        return "touch", int(merge_every_jobs or max(1, int(jobs_per_rank)))
+    every = int(merge_every_jobs or DP_TOUCH_EVERY_JOBS)
+    if pairs_per_rank >= DP_TOUCH_FIXED_PAIRS:
+        return "touch", every
     per_epoch = max(1, -(-int(jobs_per_rank) // DP_MERGES_PER_EPOCH))
     if pairs_per_rank >= DP_TOUCH_MIN_PAIRS:
-        return "touch", min(int(merge_every_jobs), per_epoch)
+        return "touch", min(every, per_epoch)
     return "align", per_epoch
 
 

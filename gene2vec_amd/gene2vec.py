@@ -236,16 +236,18 @@ def main(argv=None):
                         help="load every iteration's model back from the checkpoint just "
                              "written, as src/gene2vec.py:86 does (the kept in-memory model "
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
-    parser.add_argument("--merge-every-jobs", type=int, default=3584,
-                        help="data-parallel replica merge cadence of the touch rule (gensim "
-                             "jobs per rank; 3584 = 7 merges per epoch at C3, DESIGN.md 7a)")
+    parser.add_argument("--merge-every-jobs", type=int, default=None,
+                        help="data-parallel replica merge cadence (gensim jobs per rank); "
+                             "default: the plan's -- once per epoch up to 4 ranks, every 3,584 "
+                             "jobs (7 merges per epoch at C3) beyond (DESIGN.md 7a)")
     parser.add_argument("--merge-rule", choices=("auto", "touch", "align", "mean"),
                         default="auto",
-                        help="data-parallel replica merge rule: auto = touch every "
-                             "--merge-every-jobs jobs from 125 M pairs per rank, touch at 7 "
-                             "merges per epoch from 80 M, align at 7 merges per epoch below "
-                             "(only with a lowered --dp-min-pairs-per-rank; DESIGN.md 7a/7b); "
-                             "an explicit rule uses --merge-every-jobs")
+                        help="data-parallel replica merge rule: auto = touch once per epoch "
+                             "up to 4 ranks; beyond, touch every --merge-every-jobs jobs from "
+                             "125 M pairs per rank, touch at 7 merges per epoch from 80 M, align "
+                             "at 7 merges per epoch below (only with a lowered "
+                             "--dp-min-pairs-per-rank; DESIGN.md 7a/7b); an explicit rule uses "
+                             "--merge-every-jobs (default 3,584)")
     parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
                         default="auto",
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
@@ -374,7 +376,8 @@ def main(argv=None):
         import gene2vec_amd.word2vec as W
         from . import distributed as Dd
         W.DP_MERGE_RULE, W.DP_MERGE_EVERY_JOBS = Dd.dp_merge_plan(
-            n_pairs / max(1, dworld), args.merge_every_jobs, args.merge_rule)
+            n_pairs / max(1, dworld), args.merge_every_jobs, args.merge_rule,
+            jobs_per_rank=-(-(-(-n_pairs // max(1, dworld))) // 5000), world=dworld)
         if shard:
             print(f"data parallel: {dworld} ranks x {n_pairs // dworld} pairs, {W.DP_MERGE_RULE} "
                   f"merge every {W.DP_MERGE_EVERY_JOBS} jobs")

@@ -189,9 +189,12 @@ class Study:
     per-iteration permutations every arm shares."""
 
     def __init__(self, R, per, V0, rep=3, modules=0, p_in=0.0, zipf=1.0, iters=10, D=200, K=5,
-                 sample=1e-3, perm_seed=11, device=0):
+                 sample=1e-3, perm_seed=11, device=0, engine_options=None):
         import torch
         self.R, self.D, self.K, self.sample, self.iters = R, D, K, sample, iters
+        # {g2v option key: value} set on every engine of both arms (e.g. the
+        # G2V_OPT_TAIL_STORE experiment, DESIGN.md 5e)
+        self.engine_options = dict(engine_options or {})
         self.V0, self.modules, self.zipf = V0, modules, zipf
         pairs, names, pos = build_corpus(R, per, V0, rep, modules, p_in, zipf)
         self.n = n = len(pairs)
@@ -248,6 +251,8 @@ class Study:
     def train_single(self, seed=1, progress=None):
         eng = E.SGNSEngine(self.V, self.D, self.K)
         try:
+            for k, v in self.engine_options.items():
+                eng.set_option(k, v)
             eng.set_vocab(self.vc, self.sample)
             eng.set_weights(self.syn0, np.zeros_like(self.syn0))
             rs = np.random.RandomState(seed)
@@ -274,6 +279,8 @@ class Study:
         try:
             for _ in range(R):
                 e = E.SGNSEngine(self.V, self.D, self.K)
+                for k, v in self.engine_options.items():
+                    e.set_option(k, v)
                 e.set_vocab(self.vc, self.sample)
                 e.set_weights(self.syn0, np.zeros_like(self.syn0))
                 e.set_option(N.OPT_MERGE_BETA_MILLI, beta)

@@ -91,6 +91,9 @@ typedef struct g2v_stats {
     /* waves that trained in that launch (ABI 4): sgns_grid x the active waves,
      * fewer where the stability cap held them back */
     int64_t sgns_waves;
+    /* first syn0 / syn1neg row that launch wrote with plain stores instead of
+     * float atomics (G2V_OPT_TAIL_STORE; ABI 5), -1 = none */
+    int64_t tail_row_syn0, tail_row_syn1neg;
 } g2v_stats;
 
 /* ---- errors / version --------------------------------------------------- */
@@ -135,7 +138,10 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         its segment SHARES are).  The throughput ablations
  *                         1, 3, 4, 5, 6, 7, 9 (profiles/r0*)
  *                         exist only in the -DG2V_ABLATIONS build
- *                         (gene2vec_amd.build.build(ablations=True)); any
+ *                         (gene2vec_amd.build.build(ablations=True)), with
+ *                         10 = the lost-update probe of the tail stores
+ *                         (g2v_debug_stamps [14] stores, [15] rows another
+ *                         wave had changed before the store landed); any
  *                         mode this library does not compile, or a shape it
  *                         is not compiled for, is G2V_EINVAL [0]
  *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
@@ -173,14 +179,19 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         runs its chunks in record order, a deterministic
  *                         update order (parity checks) [4]
  *   G2V_OPT_TAIL_STORE    Hogwild kernel, vector_size <= 256 and negative <= 7
- *                         (experiment): rows with index >= n
- *                         (never a striped row) of an example without a
- *                         repeated target take plain write-through stores of
- *                         their new value instead of float atomics of the
- *                         delta -- gensim's own unsynchronised read-modify-
- *                         write, which loses an update when another wave
- *                         wrote the row between this wave's read and its
- *                         store; 0 = off [0]
+ *                         (DESIGN.md 5e): cold rows (never a striped row;
+ *                         syn1neg rows only in an example without a repeated
+ *                         target) take plain write-through stores of their
+ *                         new value instead of float atomics of the delta --
+ *                         gensim's own unsynchronised read-modify-write, which
+ *                         loses an update when another wave wrote the row
+ *                         between this wave's read and its store.  -1 = auto:
+ *                         the syn1neg rows other in-flight waves rarely touch
+ *                         (waves x the row's updates per example <= 0.15,
+ *                         from the vocabulary of g2v_set_vocab; none at <=
+ *                         ~5,000 genes), syn0 (the exported vectors) all
+ *                         atomic; n > 0 = rows >= n of both tables, 0 = off;
+ *                         g2v_stats reports the rows a launch used [-1]
  *   (keys 19 and 20, G2V_OPT_ATOMIC_TAILS / G2V_OPT_COPY_DEFER of ABI 4, were
  *    retired in ABI 5: both measured slower; G2V_EINVAL)
  *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the

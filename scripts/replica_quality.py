@@ -57,19 +57,26 @@ def main():
     ap.add_argument("--oracle", action="store_true",
                     help="also train the sequential C oracle (gensim workers=1 order) on the same "
                          "permutations and job seeds as the first one-model run")
+    ap.add_argument("--ensemble-singles", action="store_true",
+                    help="also score the plain average of the one-model runs' tables (the "
+                         "ensemble effect of averaging independently trained models)")
+    ap.add_argument("--tail-store", type=int, default=0,
+                    help="G2V_OPT_TAIL_STORE on every engine (experiment, DESIGN.md 5e)")
     ap.add_argument("--out", default="gpurun_out/replica_quality")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     K, D = a.negative, a.dim
     t0 = time.time()
+    from gene2vec_amd import _native as N
     st = RQ.Study(a.replicas, a.pairs_per_replica, a.vocab, a.ggipnn_repeat, a.modules,
-                  a.p_module, a.zipf, a.iters, D, K, a.sample)
+                  a.p_module, a.zipf, a.iters, D, K, a.sample,
+                  engine_options={N.OPT_TAIL_STORE: a.tail_store} if a.tail_store else None)
     gmt = st.gmt(os.path.join(a.out, "synthetic.gmt"))
     log = {"config": {"replicas": a.replicas, "pairs_per_replica": a.pairs_per_replica,
                       "ggipnn_repeat": a.ggipnn_repeat, "modules": a.modules,
                       "p_module": a.p_module if a.modules else 0.0, "zipf": a.zipf,
                       "pairs_total": st.n, "vocab": st.V, "dim": D, "negative": K,
-                      "sample": a.sample, "iters": a.iters},
+                      "sample": a.sample, "iters": a.iters, "tail_store": a.tail_store},
            "corpus_s": round(time.time() - t0, 1), "runs": {}}
     print(json.dumps(log["config"]), flush=True)
     auc_seeds = [int(x) for x in a.auc_seeds.split(",")]
@@ -99,6 +106,7 @@ def main():
         json.dump(log, open(os.path.join(a.out, "replica_quality.json"), "w"), indent=1)
 
     # ---- one model over the whole corpus ----------------------------------------
+    singles = []
     for si, sseed in enumerate(int(x) for x in a.single_seeds.split(",")):
         if a.no_single:
             break
@@ -107,6 +115,14 @@ def main():
         t = time.time()
         s0, s1 = st.train_single(sseed, progress=cb)
         finish(tag, s0, s1, {"train_s": round(time.time() - t, 1), "heldin_per_iter": per_it})
+        if a.ensemble_singles:
+            singles.append((s0, s1))
+    if len(singles) > 1:
+        # the models trained independently (their own job seeds, the same
+        # permutations), averaged once at the end: no merge during training
+        e0 = np.mean([x[0] for x in singles], axis=0, dtype=np.float64).astype(np.float32)
+        e1 = np.mean([x[1] for x in singles], axis=0, dtype=np.float64).astype(np.float32)
+        finish("single_ensemble", e0, e1, {"members": len(singles)})
 
     # ---- the sequential oracle (gensim's workers=1 order) -----------------------------
     if a.oracle:

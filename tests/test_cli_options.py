@@ -23,7 +23,7 @@ def test_cli_defaults_match_the_c3_gate():
     jobs from 125 M pairs per rank and sharding from 50 M; the reference's own settings
     (src/gene2vec.py:57-63) stay the CLI's"""
     a = _parsed(["d", "o", "txt"])
-    assert a["merge_every_jobs"] == 3584 and a["dp_min_pairs_per_rank"] == 80_000_000
+    assert a["merge_every_jobs"] is None and a["dp_min_pairs_per_rank"] == 80_000_000
     assert a["merge_rule"] == "auto"
     assert (a["dim"], a["negative"], a["window"], a["sample"], a["iters"], a["workers"]) == \
         (200, 5, 1, 1e-3, 10, 32)
@@ -58,3 +58,18 @@ def test_dp_merge_plan_by_shard_size():
     assert Dd.dp_merge_plan(100_000_000, 1000) == ("touch", 1000)
     assert Dd.dp_merge_plan(50_000_000, 4096, "touch") == ("touch", 4096)
     assert Dd.dp_merge_plan(60_000_000, 333, "mean") == ("mean", 333)
+    assert Dd.dp_merge_plan(60_000_000, None, "mean") == ("mean", 3584)
+
+
+def test_dp_merge_plan_by_world_size():
+    """up to 4 ranks the plan merges once per epoch (DESIGN.md 7a, round 5:
+    the least target-function lead over one model at 2 and 4 ranks); 8 ranks
+    keep the C3 plan; an explicit cadence wins"""
+    from gene2vec_amd import distributed as Dd
+    for w in (2, 3, 4):
+        assert Dd.dp_merge_plan(125_000_000, world=w) == ("touch", 25_000)
+        assert Dd.dp_merge_plan(80_000_000, world=w) == ("touch", 16_000)
+        assert Dd.dp_merge_plan(125_000_000, 3584, world=w) == ("touch", 3584)
+    assert Dd.dp_merge_plan(125_000_000, world=5) == ("touch", 3584)
+    assert Dd.dp_merge_plan(125_000_000, world=8) == ("touch", 3584)
+    assert Dd.dp_merge_plan(125_000_000, jobs_per_rank=25_088, world=4) == ("touch", 25_088)

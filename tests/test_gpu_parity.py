@@ -438,9 +438,16 @@ def test_train_hogwild_full_vocab_tracks_oracle():
                  CO.sample_int(counts, sample), True, CO.make_cum_table(counts), a0, a1,
                  np.ones(V, np.float32), K)
     g0, g1 = eng.get_weights()
+    st = eng.read_stats()
     l_gpu = _eval_loss(g0, g1, tok, counts, K, n_eval=50000)
     l_ref = _eval_loss(a0, a1, tok, counts, K, n_eval=50000)
     assert abs(l_gpu - l_ref) / l_ref < 0.003, (l_gpu, l_ref)
+    # the default cold-row stores (G2V_OPT_TAIL_STORE auto): at
+    # 1,024 waves the collision budget (waves x updates per example <= 0.15)
+    # starts syn1neg at row ~7,700 for this vocabulary; syn0 stays atomic
+    assert st["sgns_grid"] == 256
+    assert 7000 < st["tail_row_syn1neg"] < 8500, st
+    assert st["tail_row_syn0"] == -1, st
 
 
 def test_striping_keeps_values_exact():

@@ -47,6 +47,7 @@ def standin():
 
 def _env(standin, **extra):
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", G2V_RCCL_LIB=standin,
+               G2V_ALLOW_RCCL_STANDIN="1",
                G2V_RCCL_STANDIN_MB="64", G2V_RCCL_STANDIN_TIMEOUT_S="90",
                PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     env.update(extra)
