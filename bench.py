@@ -42,6 +42,7 @@ METRIC = "gene pairs/sec (SGNS dim200 neg5) at 1/2/4/8 MI355X + achieved GB/s"
 # BASELINE.json configs[3] (C4): python bench.py --vocab 60000 --dim 512 --negative 15
 HBM_PEAK_GBPS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 ATOMIC_PEAK_GBPS = 1300.0  # MI355X_MICROARCH.md "Global float atomics": chip-wide added bytes
+STORE_PEAK_GBPS = 6100.0  # same section: plain dword stores of the same shape, 6.0-6.2 TB/s
 
 
 def usable_cpus():
@@ -414,24 +415,49 @@ def main():
                        "this workload"
                        + (f"; refused profiles of other builds: {', '.join(stale[:3])}"
                           if stale else ""))
-    atomic_bytes = (K + 2) * D * 4  # every SGNS update is a memory-side f32 atomic delta
-    atomic_gbps = atomic_bytes * st["examples"] / (st["sgns_kernel_ms"] / 1e3) / 1e9 \
-        if st["sgns_kernel_ms"] > 0 else 0.0
-    # bound = the resource that binds k_sgns_atomic: every table update is a
-    # memory-side f32 atomic (MI355X_MICROARCH.md "Global float atomics": ~1.3
-    # TB/s of added bytes chip-wide, whatever the placement); achieved = the
-    # algorithmic atomic bytes (K+2)*D*4 per directed example / launch time.
+    # bound = the resource that binds k_sgns_atomic: its row updates leave the
+    # CU as memory-side f32 atomics of the delta (MI355X_MICROARCH.md "Global
+    # float atomics": ~1.3 TB/s of added bytes chip-wide, whatever the
+    # placement) except the cold syn1neg rows' plain write-through stores of
+    # the new value (G2V_OPT_TAIL_STORE; the guide's plain
+    # stores of the same shape: 6.0-6.2 TB/s).  Per directed example
+    # (K+2)*D*4 algorithmic update bytes; the stored share is the vocabulary's
+    # expectation for the rows the launches stored (g2v_stats tail rows: the
+    # centre and K negatives of syn1neg from p_tok / p_neg, the syn0 input
+    # from p_tok; checked against the lost-update probe's store count).  The
+    # roof time is atomic bytes / 1.3 TB/s + stored bytes / 6.1 TB/s;
+    # achieved = update bytes / launch time, peak = update bytes / roof time.
     # The HBM view of the same launches (2*(K+2)*D*4 bytes per example: every
     # updated row read and written) stays beside it as hbm_*.
-    roofline = {"bound": "atomics", "achieved": round(atomic_gbps, 1), "peak": ATOMIC_PEAK_GBPS,
-                "unit": "GB/s", "frac": round(atomic_gbps / ATOMIC_PEAK_GBPS, 4),
+    update_bytes = (K + 2) * D * 4
+    pt_r = E.kept_token_share(vcounts, a.sample)
+    pn_r = vcounts.astype(np.float64) ** 0.75
+    pn_r /= pn_r.sum()
+    t0r, t1r = st["tail_row_syn0"], st["tail_row_syn1neg"]
+    stored_rows = ((pt_r[t1r:].sum() + K * pn_r[t1r:].sum()) if t1r >= 0 else 0.0) \
+        + (pt_r[t0r:].sum() if t0r >= 0 else 0.0)
+    stored_bytes = stored_rows * D * 4
+    atomic_bytes = update_bytes - stored_bytes
+    t_ex = st["sgns_kernel_ms"] / 1e3 / max(1, st["examples"])  # s per example
+    roof_t_ex = atomic_bytes / (ATOMIC_PEAK_GBPS * 1e9) + stored_bytes / (STORE_PEAK_GBPS * 1e9)
+    upd_gbps = update_bytes / t_ex / 1e9 if t_ex > 0 else 0.0
+    peak_gbps = update_bytes / roof_t_ex / 1e9
+    roofline = {"bound": "atomics", "achieved": round(upd_gbps, 1), "peak": round(peak_gbps, 1),
+                "unit": "GB/s", "frac": round(upd_gbps / peak_gbps, 4),
                 "traffic": traffic,
                 "kernel": "k_sgns_atomic", "avg_launch_ms": round(avg_launch_ms, 4),
-                "atomic_bytes_per_example": atomic_bytes,
+                "update_bytes_per_example": update_bytes,
+                "atomic_bytes_per_example": round(atomic_bytes, 1),
+                "stored_bytes_per_example": round(stored_bytes, 1),
+                "stored_rows_per_example": round(float(stored_rows), 4),
+                "atomic_achieved_GBps": round(atomic_bytes / t_ex / 1e9, 1) if t_ex > 0 else 0.0,
+                "atomic_peak_GBps": ATOMIC_PEAK_GBPS, "store_peak_GBps": STORE_PEAK_GBPS,
                 "algorithmic_bytes_per_launch": int(alg_bytes_launch),
                 "bytes_per_example": bytes_per_example,
                 "binding_resource": "memory-side float atomics (MI355X_MICROARCH.md: ~1300 GB/s "
-                                    "of added bytes chip-wide)",
+                                    "of added bytes chip-wide) plus the cold rows' plain stores "
+                                    "(~6100 GB/s); peak = the update bytes over "
+                                    "atomic/1300 + stored/6100",
                 "hbm_achieved_GBps": round(achieved, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
                 "hbm_frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",

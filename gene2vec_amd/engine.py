@@ -90,6 +90,22 @@ def first_occurrence_perm8(device, items_ptr, n_items, seed, n_ids, first_ptr, s
                                                C.c_void_p(stream) if stream else None))
 
 
+def kept_token_share(counts, sample):
+    """each row's share of the tokens downsampling keeps ([ext] prepare_vocab's
+    sample_int as a probability, Appendix A.2; the p_tok(r) g2v_set_vocab
+    derives the Hogwild budgets and the tail-store rows from)"""
+    v = np.asarray(counts, dtype=np.float64)
+    total = v.sum()
+    if 0.0 < sample < 1.0:
+        thr = sample * total
+    elif sample >= 1.0:
+        thr = float(int(sample * (3.0 + np.sqrt(5.0)) / 2.0))
+    else:
+        thr = total
+    kept = v * np.minimum(1.0, (np.sqrt(v / thr) + 1.0) * (thr / v))
+    return kept / kept.sum()
+
+
 def count_ids(ids, V):
     ids = np.ascontiguousarray(ids, dtype=np.int32)
     counts = np.zeros(V, dtype=np.int64)

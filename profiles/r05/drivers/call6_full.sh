@@ -2,7 +2,7 @@
 # round 5: the whole GPU suite on the current tree, then the default bench and smoke()
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05c6
+O=gpurun_out/r05c10
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 700 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/gpu_tests.log | tail -5

@@ -12,9 +12,11 @@ Means over the same three model.random seeds; bars 1 % (north star) for the
 final-iteration loss and the manuscript target function
 (src/evaluation_target_function.py, planted modules as pathways) and 0.5 %
 for the SGNS objective on corpus pairs.  The Hogwild staleness shows in the
-target function most (-0.7 % here, -1.4 % on a denser
-10 k-gene corpus, -0.25 % at the C2 vocabulary; gensim's own 32-thread
-Hogwild, restated, sits 0.1-0.8 % below its sequential order)."""
+target function most (round 5, the production kernel
+with its cold syn1neg rows stored: -0.5 % here, -0.3 % at the C2 vocabulary,
+-0.8 % on the dense 5,000-gene corpus with syn0 stores too, which is why syn0
+stays atomic; round 4, all atomics: -0.25 / -0.09 / -0.46 %; gensim's own
+32-thread Hogwild, restated, sits 0.1-0.8 % below its sequential order)."""
 import json
 import os
 import zlib
@@ -127,8 +129,10 @@ def test_gpu_end_to_end_at_the_c2_vocabulary(tmp_path):
     """the same gate at the bench's vocabulary (24,447 Zipf genes, 1,000
     planted modules, 10 M pairs, sample 1e-3), the production defaults (one
     workgroup per CU); golden from the sequential oracle, two seeds
-    (tests/golden/make_e2e_golden.py --c2).  Measured: loss +0.06 %,
-    objective -0.05 %, target function -0.15 %."""
+    (tests/golden/make_e2e_golden.py --c2).  The only e2e corpus with
+    syn1neg rows cold enough for the default tail stores.
+    Measured, round 5: loss +0.4 %, objective +0.29 %, target function
+    -0.3 % (all atomics, round 4: +0.07 / -0.05 / -0.09 %)."""
     ref = _golden("e2e_parity_c2.json", E2E_C2)
     got = _train_e2e(tmp_path, E2E_C2["sample"], cfg=E2E_C2)
     gaps = _gaps(got, ref)
@@ -143,7 +147,8 @@ def test_gpu_end_to_end_dense_5k_genes(tmp_path):
     (5,000 genes, 200 planted modules, 4 M pairs: every gene in ~1,600 pairs;
     DESIGN.md 8 measured -0.97 % at the default one-workgroup-per-CU grid with
     GGIPNN pairs added, -1.39 % at the 295 workgroups the staleness budget
-    alone allowed).  Golden: the sequential oracle, three seeds
+    alone allowed; rounds 4 and 5 -0.46 % with all rows atomic, -0.84 % when
+    syn0 rows were stored too).  Golden: the sequential oracle, three seeds
     (tests/golden/make_e2e_golden.py --v5k).  North-star bar: 1 % on the loss
     and the target function, 0.5 % on the SGNS objective."""
     ref = _golden("e2e_parity_v5k.json", E2E_V5K)
