@@ -26,6 +26,10 @@ SOURCES = sorted({u[0] for u in UNITS})
 HEADERS = [os.path.join(CSRC, "g2v_internal.h"), os.path.join(CSRC, "g2v_device.h"),
            os.path.join(ROOT, "include", "g2v.h")]
 ARCH = "gfx950"
+# k_sgns_atomic's store-or-atomics choice per row is a uniform if / else that
+# must stay a diamond for the loop head to wait with vmcnt(#row instructions)
+# instead of vmcnt(0) (g2v_sgns_atomic.hip; tests/test_kernel_isa.py)
+SGNS_KERNEL_FLAGS = ("-mllvm", "-structurizecfg-skip-uniform-regions=true")
 # the sources that determine k_sgns_atomic's code (bench.py accepts a PMC
 # traffic profile only when it was measured on this exact kernel code AND the
 # same launch layout: grid and stripe tiers, recorded beside the hash)
@@ -65,14 +69,24 @@ def _stale(lib=LIB) -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False, ablations: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, ablations: bool = False,
+          defines=(), tag: str = "", kernel_flags=()) -> str:
     """Compile every translation unit in parallel (one hipcc per file), then link.
-    ablations=True: the -DG2V_ABLATIONS library (ABLATIONS_LIB) instead."""
-    out = ABLATIONS_LIB if ablations else LIB
+    ablations=True: the -DG2V_ABLATIONS library (ABLATIONS_LIB) instead;
+    tag + defines: an experiment build gene2vec_amd/libg2v_exp_<tag>.so with
+    extra -D flags and extra compiler flags for the SGNS-kernel units
+    (kernel_flags; A/B scripts load it with _native.use_library; never the
+    product)"""
+    if tag:
+        out = os.path.join(HERE, f"libg2v_exp_{tag}.so")
+        objdir = os.path.join(HERE, "build", f"exp_{tag}")
+    elif ablations:
+        out, objdir = ABLATIONS_LIB, os.path.join(HERE, "build", "ablations")
+    else:
+        out, objdir = LIB, os.path.join(HERE, "build")
     if not force and not _stale(out):
         return out
     from concurrent.futures import ThreadPoolExecutor
-    objdir = os.path.join(HERE, "build", "ablations") if ablations else os.path.join(HERE, "build")
     os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              # IEEE semantics: every fused multiply-add in the kernels is explicit
@@ -80,6 +94,7 @@ def build(force: bool = False, verbose: bool = False, ablations: bool = False) -
              "-I", os.path.join(ROOT, "include"), "-I", CSRC]
     if ablations:
         flags.append("-DG2V_ABLATIONS")
+    flags += [f"-D{d}" for d in defines]
     objs = [os.path.join(objdir, u[2]) for u in UNITS]
 
     def compile_one(i):
@@ -88,7 +103,8 @@ def build(force: bool = False, verbose: bool = False, ablations: bool = False) -
         if (not force and os.path.exists(objs[i])
                 and all(os.path.getmtime(d) <= os.path.getmtime(objs[i]) for d in deps)):
             return ""
-        cmd = [hipcc(), *flags, *defs, "-c", os.path.join(CSRC, src), "-o", objs[i]]
+        kf = (list(SGNS_KERNEL_FLAGS) + list(kernel_flags)) if src == "g2v_sgns_atomic.hip" else []
+        cmd = [hipcc(), *flags, *kf, *defs, "-c", os.path.join(CSRC, src), "-o", objs[i]]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -1198,7 +1198,8 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   s.stripe2 = c->stripe2;
   // cold-row plain stores (G2V_OPT_TAIL_STORE), never on a striped row
   s.tail_row0 = s.tail_row1 = 0x7fffffff;
-  if (atomic_kernel && (c->debug_write == 0 || c->debug_write == 10) && c->nv == 1 &&
+  if (atomic_kernel && (c->debug_write == 0 || c->debug_write == 8 || c->debug_write == 10) &&
+      c->nv == 1 &&
       c->K + 1 <= 8 && c->tail_store != 0) {
     int t0 = c->tail_store, t1 = c->tail_store;
     if (c->tail_store < 0) {

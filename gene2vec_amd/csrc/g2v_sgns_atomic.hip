@@ -33,7 +33,12 @@ namespace g2v {
 // scripts/stamp_segments.py).  The throughput ablations (WR 1, 3, 4, 5, 9 and
 // G2V_OPT_DEBUG_WRITE 6 / 7) exist only in the -DG2V_ABLATIONS build
 // (gene2vec_amd.build.build(ablations=True) -> gene2vec_amd/libg2v_ablations.so).
-constexpr int kStripeBatch = 7;
+// copies of a striped row requested per load batch: all 15 of the top tier's
+// extra copies at once for D <= 256 (one memory latency per row instead of
+// three; round 5, interleaved A/B: C2 +0.9 %, sample 0 +0.5-1.6 %; round 2's
+// kernel had measured no difference), 7 at D > 256 (twice the registers)
+template <int NV>
+constexpr int stripe_batch() { return NV == 1 ? 15 : 7; }
 constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
 
 template <int K, int NV>
@@ -65,14 +70,15 @@ __device__ __forceinline__ void load_main(float4 (&o)[NV], __amdgpu_buffer_rsrc_
 }
 
 // ... plus its stripe copies when t is a striped hot row (t < stripe_rows).
-// The copies are loaded kStripeBatch at a time and summed in copy order, so a
-// striped row costs one memory latency per batch, not one per copy; copies
+// The copies are loaded stripe_batch() at a time and summed in copy order, so
+// a striped row costs one memory latency per batch, not one per copy; copies
 // past stripe_copies read an out-of-range offset (zeros, no memory access).
 // t: the row's index within its tier, rows / C: the tier's row count and copies
 template <int NV>
 __device__ __forceinline__ void add_stripes(float4 (&o)[NV], __amdgpu_buffer_rsrc_t rs, int t,
                                             int tbl, int rows, int C, int rowb,
                                             const uint32_t (&loff)[NV]) {
+  constexpr int kStripeBatch = stripe_batch<NV>();
   for (int c0 = 1; c0 < C; c0 += kStripeBatch) {
     float4 q[kStripeBatch][NV];
 #pragma unroll
@@ -356,9 +362,9 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int NT = K + 1;
   constexpr int W = kSgnsThreads / 64;
   constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
-  // tail stores compiled in (WR 10, ablation build: the same, with the
-  // lost-update probe)
-  constexpr bool TS = (WR == 0 || WR == 10) && tail_ok<K, NV>();
+  // tail stores compiled in (WR 8: the stamped production build; WR 10,
+  // ablation build: with the lost-update probe)
+  constexpr bool TS = (WR == 0 || WR == 8 || WR == 10) && tail_ok<K, NV>();
   __shared__ float s_lut[kExpTableSize];
   __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
@@ -679,18 +685,20 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         continue;
       }
 #endif
-      // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work.
-      // A row stored instead (G2V_OPT_TAIL_STORE) still issues its 4 NV
-      // atomics, dropped by an empty resource, and THEN its stores: every
-      // path issues at least the same 4 NV (K + 2) instructions after the
-      // next example's loads, so the loop head keeps waiting with
-      // vmcnt(#atomics) (an if / else of stores or atomics is lowered to two
-      // triangles, and the path through neither made it wait with vmcnt(0))
+      // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work;
+      // a cold row (G2V_OPT_TAIL_STORE) takes its 4 NV stores INSTEAD: a
+      // uniform if / else with 4 NV vector-memory instructions on each side,
+      // so the loop head waits for the next example's loads with
+      // vmcnt(#row instructions).  That needs the build's
+      // -structurizecfg-skip-uniform-regions (gene2vec_amd/build.py): the
+      // default structurizer lowers the if / else to two triangles, and the
+      // path through neither made the loop head wait with vmcnt(0) (every
+      // atomic of the previous example drained before the next compute);
+      // tests/test_kernel_isa.py checks the wait in the assembly
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         float* row = upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb);
         const bool st = uniform_b(TS && !rep && tg[d] >= tail1);
-        emit_row<NV, WR>(row, live[d] && !st, D, v1, g[d], lane);
         if (st) {
           float val[4 * NV];
 #pragma unroll
@@ -699,13 +707,14 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           if (WR == 10 && live[d]) lost_probe(row, s_to[wid][d * 64 + lane], a.stamps, lane);
 #endif
           store_row<NV>(row, live[d], D, val, lane);
+        } else {
+          emit_row<NV, WR>(row, live[d], D, v1, g[d], lane);
         }
         if (WR == 8 && d == 3) sub[2] += stamp_time() - ts;  // 16 atomics issued
       }
       {
         float* row = upd_row<WR>(a, 0, input, cbase + NT, rowb);
         const bool st = uniform_b(TS && input >= tail0);
-        emit_row<NV, WR>(row, any && !st && WR != 5, D, vw, lf, lane);
         if (st) {
           float val[4 * NV];
 #pragma unroll
@@ -714,6 +723,8 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
           if (WR == 10 && any) lost_probe(row, v1[0], a.stamps, lane);
 #endif
           store_row<NV>(row, any, D, val, lane);
+        } else {
+          emit_row<NV, WR>(row, any && WR != 5, D, vw, lf, lane);
         }
       }
       __builtin_amdgcn_wave_barrier();

@@ -44,12 +44,17 @@ def main():
                          "G2V_OPT_TAIL_STORE N), stamped_tailN, any suffix _again; notail "
                          "needs the ablation build (--ablations)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--library", default=None,
+                    help="load this libg2v build instead (an experiment build, "
+                         "gene2vec_amd.build.build(tag=..., defines=...))")
     ap.add_argument("--ablations", action="store_true",
                     help="load the -DG2V_ABLATIONS build (debug write modes 1, 3-7, 9)")
     a = ap.parse_args()
     if a.ablations:
         from gene2vec_amd import build as B
         N.use_library(B.build(ablations=True))
+    elif a.library:
+        N.use_library(a.library)
     D, K = 200, 5
     pairs = S.zipf_gene_pairs(a.pairs, a.vocab, 1.0, seed=20250114)
     flat = pairs.reshape(-1)
@@ -78,7 +83,9 @@ def main():
         dbg = 8 if base.startswith("stamped") else {"notail": 9}.get(base, 0)
         eng.set_option(N.OPT_DEBUG_WRITE, dbg)
         eng.set_option(N.OPT_STRIPE_COPIES, int(base[6:]) if base.startswith("copies") else 0)
-        tail = base.split("tail")[-1] if "tail" in base and base != "notail" else "0"
+        # tailN: G2V_OPT_TAIL_STORE N (tail0 = all atomic); otherwise the
+        # library's default (-1, the collision budget)
+        tail = base.split("tail")[-1] if "tail" in base and base != "notail" else "-1"
         eng.set_option(N.OPT_TAIL_STORE, int(tail))
         eng.train(js, al, E.job_seeds(rs, len(js) - 1), N.MODE_HOGWILD)  # warm (and |syn1| grows)
         eng.read_stats()
