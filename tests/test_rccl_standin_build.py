@@ -27,13 +27,19 @@ class Uid(C.Structure):
     _fields_ = [("internal", C.c_char * 128)]
 
 
-def _rank(path, uid_bytes, rank, q, abort):
+def _rank(path, uid_bytes, rank, q, abort, inited):
     lib = C.CDLL(path)
     comm = C.c_void_p()
     uid = Uid.from_buffer_copy(uid_bytes)
     rc = lib.ncclCommInitRank(C.byref(comm), 2, uid, rank)
     q.put((rank, "init", rc))
+    inited[rank].set()
     if rc == 0:
+        if abort:
+            # abort only once the peer is out of its init barrier: an abort
+            # while it still waits there fails its init (the stand-in's
+            # documented semantics), which is not what this test checks
+            inited[1 - rank].wait(60)
         rc2 = (lib.ncclCommAbort if abort else lib.ncclCommDestroy)(comm)
         q.put((rank, "end", rc2))
 
@@ -46,7 +52,9 @@ def test_two_processes_form_and_leave_a_communicator():
     assert uid.internal.startswith(b"/g2v_rccl_standin_")
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank, args=(path, bytes(uid), r, q, r == 1)) for r in range(2)]
+    inited = [ctx.Event(), ctx.Event()]
+    ps = [ctx.Process(target=_rank, args=(path, bytes(uid), r, q, r == 1, inited))
+          for r in range(2)]
     for p in ps:
         p.start()
     got = [q.get(timeout=60) for _ in range(4)]
