@@ -450,6 +450,7 @@ def main():
                 "atomic_bytes_per_example": round(atomic_bytes, 1),
                 "stored_bytes_per_example": round(stored_bytes, 1),
                 "stored_rows_per_example": round(float(stored_rows), 4),
+                "tail_row_syn1neg": t1r, "tail_row_syn0": t0r,
                 "atomic_achieved_GBps": round(atomic_bytes / t_ex / 1e9, 1) if t_ex > 0 else 0.0,
                 "atomic_peak_GBps": ATOMIC_PEAK_GBPS, "store_peak_GBps": STORE_PEAK_GBPS,
                 "algorithmic_bytes_per_launch": int(alg_bytes_launch),

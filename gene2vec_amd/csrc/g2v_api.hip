@@ -759,8 +759,6 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
     case G2V_OPT_TAIL_STORE:
       REQUIRE(value >= -1 && value <= c->V, G2V_EINVAL, "tail store row %lld out of [-1, V]",
               (long long)value);
-      REQUIRE(value <= 0 || (c->nv == 1 && c->K + 1 <= 8), G2V_EINVAL,
-              "tail stores need vector_size <= 256 and negative <= 7");
       c->tail_store = (int)value;
       return G2V_OK;
     case G2V_OPT_DEBUG_FAIL_MERGE:
@@ -1199,8 +1197,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   // cold-row plain stores (G2V_OPT_TAIL_STORE), never on a striped row
   s.tail_row0 = s.tail_row1 = 0x7fffffff;
   if (atomic_kernel && (c->debug_write == 0 || c->debug_write == 8 || c->debug_write == 10) &&
-      c->nv == 1 &&
-      c->K + 1 <= 8 && c->tail_store != 0) {
+      c->tail_store != 0) {
     int t0 = c->tail_store, t1 = c->tail_store;
     if (c->tail_store < 0) {
       // auto: the collision budget over the waves this launch may run

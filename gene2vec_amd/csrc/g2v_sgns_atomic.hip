@@ -352,10 +352,10 @@ __device__ __forceinline__ int64_t next_chunk(unsigned int* q, int lane) {
   return (int64_t)__builtin_amdgcn_readfirstlane(v);
 }
 
-// tail stores stage the new syn1neg rows in LDS: NV = 1 and K + 1 <= kTailMaxRows
-constexpr int kTailMaxRows = 8;
-template <int K, int NV>
-constexpr bool tail_ok() { return NV == 1 && K + 1 <= kTailMaxRows; }
+// tail stores stage the new values of up to kTailSlots cold syn1neg rows per
+// example in LDS (later cold rows of the example take atomics): 6 KB per wave
+// at negative 5 / D <= 256, 16 KB at D > 256 with 8 or more targets
+constexpr int kTailSlots = 8;
 
 template <int K, int NV, int WR = 0, bool LOSS = false>
 __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
@@ -364,13 +364,14 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   constexpr int RS = (3 + K + 3) / 4 * 4;  // record stride (g2v_create: 16-B records)
   // tail stores compiled in (WR 8: the stamped production build; WR 10,
   // ablation build: with the lost-update probe)
-  constexpr bool TS = (WR == 0 || WR == 8 || WR == 10) && tail_ok<K, NV>();
+  constexpr bool TS = WR == 0 || WR == 8 || WR == 10;
+  constexpr int kSlots = NT < kTailSlots ? NT : kTailSlots;
   __shared__ float s_lut[kExpTableSize];
   __shared__ float s_log[LOSS ? kExpTableSize : 1];
   __shared__ float s_l1[W][256 * NV];
   __shared__ float s_wk[W][256 * NV];
-  __shared__ float s_tl[W][TS ? NT * 256 : 1];  // tail rows' new values (TS)
-  __shared__ float s_to[W][WR == 10 ? NT * 64 : 1];  // WR 10: their old first 64 floats
+  __shared__ float s_tl[W][TS ? kSlots * 256 * NV : 1];  // tail rows' new values (TS)
+  __shared__ float s_to[W][WR == 10 ? kSlots * 64 : 1];  // WR 10: their old first 64 floats
   __shared__ int32_t s_rec[W][kChunk * RS];  // the wave's chunk of records
   __shared__ float s_lf[W][kChunk];          // lockf[input] per record of the chunk
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
@@ -521,6 +522,12 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       for (int d = 1; d < NT; ++d)
 #pragma unroll
         for (int d2 = 0; d2 < d; ++d2) rep |= x.tg[d2] == x.tg[d];  // (-1 pads: general path)
+      // per target: its LDS staging slot when the row is stored (a cold row of
+      // a repeat-free example, while slots last), -1 = float atomics
+      int slot[NT];
+#pragma unroll
+      for (int d = 0; d < NT; ++d) slot[d] = -1;
+      int nslot = 0;
       if (!rep) {
 #pragma unroll
         for (int d = 0; d < NT; ++d) {
@@ -537,16 +544,20 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
             work[v].z = __fmaf_rn(gg, x.rw[d][v].z, work[v].z);
             work[v].w = __fmaf_rn(gg, x.rw[d][v].w, work[v].w);
           }
-          if (TS && x.tg[d] >= tail1) {
+          if (TS && x.tg[d] >= tail1 && nslot < kSlots) {
             // the cold row's new value, staged in element order for store_row
             if (WR == 10 && lane < 16)
-              *reinterpret_cast<float4*>(s_to[wid] + d * 64 + lane * 4) = x.rw[d][0];
-            float4 nw;
-            nw.x = __fmaf_rn(gg, x.l1[0].x, x.rw[d][0].x);
-            nw.y = __fmaf_rn(gg, x.l1[0].y, x.rw[d][0].y);
-            nw.z = __fmaf_rn(gg, x.l1[0].z, x.rw[d][0].z);
-            nw.w = __fmaf_rn(gg, x.l1[0].w, x.rw[d][0].w);
-            *reinterpret_cast<float4*>(stl + d * 256 + lane * 4) = nw;
+              *reinterpret_cast<float4*>(s_to[wid] + nslot * 64 + lane * 4) = x.rw[d][0];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+              float4 nw;
+              nw.x = __fmaf_rn(gg, x.l1[v].x, x.rw[d][v].x);
+              nw.y = __fmaf_rn(gg, x.l1[v].y, x.rw[d][v].y);
+              nw.z = __fmaf_rn(gg, x.l1[v].z, x.rw[d][v].z);
+              nw.w = __fmaf_rn(gg, x.l1[v].w, x.rw[d][v].w);
+              *reinterpret_cast<float4*>(stl + nslot * 256 * NV + (lane + 64 * v) * 4) = nw;
+            }
+            slot[d] = nslot++;
           }
           g[d] = gg;
           live[d] = true;
@@ -698,13 +709,13 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #pragma unroll
       for (int d = 0; d < NT; ++d) {
         float* row = upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb);
-        const bool st = uniform_b(TS && !rep && tg[d] >= tail1);
+        const bool st = uniform_b(TS && slot[d] >= 0);
         if (st) {
           float val[4 * NV];
 #pragma unroll
-          for (int i = 0; i < 4 * NV; ++i) val[i] = stl[d * 256 + 64 * i + lane];
+          for (int i = 0; i < 4 * NV; ++i) val[i] = stl[slot[d] * 256 * NV + 64 * i + lane];
 #ifdef G2V_ABLATIONS
-          if (WR == 10 && live[d]) lost_probe(row, s_to[wid][d * 64 + lane], a.stamps, lane);
+          if (WR == 10 && live[d]) lost_probe(row, s_to[wid][slot[d] * 64 + lane], a.stamps, lane);
 #endif
           store_row<NV>(row, live[d], D, val, lane);
         } else {

@@ -106,11 +106,11 @@ def test_one_wave_chunk_boundaries_and_short_tail():
         assert _rel(g0, r0) < 1e-5 and _rel(g1, r1) < 1e-5, (n, _rel(g0, r0), _rel(g1, r1))
 
 
-def _no_consecutive_share(V, K, n, seed):
-    """Zipf examples in which no row of either table recurs in the NEXT
-    example (the one whose loads overtake this example's writes)"""
+def _no_consecutive_share(V, K, n, seed, zipf=True):
+    """Zipf (or uniform) examples in which no row of either table recurs in
+    the NEXT example (the one whose loads overtake this example's writes)"""
     rng = np.random.RandomState(seed)
-    p = 1.0 / np.arange(1, V + 1)
+    p = 1.0 / np.arange(1, V + 1) if zipf else np.ones(V)
     p /= p.sum()
     c = np.empty(n, np.int32)
     i = np.empty(n, np.int32)
@@ -129,19 +129,20 @@ def _no_consecutive_share(V, K, n, seed):
     return c, i, negs
 
 
-@pytest.mark.parametrize("tail", [100, 1])
-def test_one_wave_tail_stores_match_restatement(tail):
+@pytest.mark.parametrize("tail,D,K", [(100, 200, 5), (1, 200, 5), (1, 512, 15)])
+def test_one_wave_tail_stores_match_restatement(tail, D, K):
     """G2V_OPT_TAIL_STORE: on one wave, with no row shared by
     consecutive examples, a cold row's plain store of (row as read + delta)
     leaves the same value as the atomic (row + delta): the kernel still
     matches orc_atomic_one_wave at 1e-5, repeated targets (atomics) included;
-    tail 1 = every unstriped row stored"""
-    V, D, K, n, alpha = 2000, 200, 5, 1500, 0.025
+    tail 1 = every unstriped row stored (at negative 15 more cold rows than
+    the 8 staging slots: the rest take atomics)"""
+    V, n, alpha = (2000, 1500, 0.025) if K == 5 else (6000, 800, 0.025)
     rng = np.random.RandomState(3)
     syn0 = ((rng.rand(V, D) - 0.5) / D).astype(np.float32)
     syn1 = ((rng.rand(V, D) - 0.5) / D * 0.1).astype(np.float32)
     lockf = np.ones(V, np.float32)
-    c, i, negs = _no_consecutive_share(V, K, n, seed=tail)
+    c, i, negs = _no_consecutive_share(V, K, n, seed=tail + K, zipf=K == 5)
     negs[5::97, 1] = negs[5::97, 0]  # some repeated targets: those examples keep atomics
     e = E.SGNSEngine(V, D, K)
     e.set_weights(syn0, syn1)
@@ -163,13 +164,14 @@ def test_one_wave_tail_stores_match_restatement(tail):
 
 
 def test_retired_and_unsupported_options_refused():
-    """ABI 5: the measured-slower kernel variants are gone (keys 19 / 20), and
-    a debug build or tail stores on a shape the library does not compile them
-    for is G2V_EINVAL, not a silent production run"""
+    """ABI 5: the measured-slower kernel variants are gone (keys 19 / 20), a
+    debug build on a shape the library does not compile it for is
+    G2V_EINVAL, not a silent production run, and tail-store rows
+    lie in [-1, V]"""
     e = E.SGNSEngine(100, 512, 15)
     try:
         for key, val in ((19, 1), (20, 1), (N.OPT_DEBUG_WRITE, 8), (N.OPT_DEBUG_WRITE, 2),
-                         (N.OPT_DEBUG_WRITE, 1), (N.OPT_TAIL_STORE, 50)):
+                         (N.OPT_DEBUG_WRITE, 1), (N.OPT_TAIL_STORE, 101), (N.OPT_TAIL_STORE, -2)):
             with pytest.raises(N.G2VError):
                 e.set_option(key, val)
     finally:
