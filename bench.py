@@ -89,9 +89,10 @@ def parse():
     p.add_argument("--sample-overlap", type=int, choices=(0, 1), default=None,
                    help="G2V_OPT_SAMPLE_OVERLAP (sampler of segment s+1 under segment s's "
                         "SGNS kernel; default: the library's)")
-    p.add_argument("--tail-store", type=int, default=0,
-                   help="G2V_OPT_TAIL_STORE: rows >= this take plain stores instead of "
-                        "atomics (experiment, DESIGN.md 5e; 0 = off, the default)")
+    p.add_argument("--tail-store", type=int, default=None,
+                   help="G2V_OPT_TAIL_STORE: -1 = the collision budget (the library's "
+                        "default), 0 = every row atomic, n = rows >= n of both tables stored "
+                        "(DESIGN.md 5e)")
     p.add_argument("--seg-jobs", type=int, default=0,
                    help="gensim jobs per sampling/update segment (0 = library default)")
     p.add_argument("--cpu-sample-pairs", type=int, default=50_000_000)
@@ -265,7 +266,7 @@ def main():
         eng.set_option(N.OPT_STRIPE2_COPIES, c2)
     if a.seg_jobs:
         eng.set_option(N.OPT_SEG_JOBS, a.seg_jobs)
-    if a.tail_store:
+    if a.tail_store is not None:
         eng.set_option(N.OPT_TAIL_STORE, a.tail_store)
     if a.sample_overlap is not None:
         eng.set_option(N.OPT_SAMPLE_OVERLAP, a.sample_overlap)

@@ -715,6 +715,13 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
 #endif
       REQUIRE(known, G2V_EINVAL, "debug write mode %lld is not compiled into this library",
               (long long)value);
+#ifdef G2V_ABLATIONS
+      // the lost-update probe also at the C4 shape (negative 15, D 257..512)
+      if (value == 10 && c->K == 15 && c->nv == 2) {
+        c->debug_write = 10;
+        return G2V_OK;
+      }
+#endif
       REQUIRE(value == 0 || (c->K == 5 && c->nv == 1), G2V_EINVAL,
               "debug write mode %lld needs negative 5 and vector_size <= 256 (have %d, %d)",
               (long long)value, c->K, c->D);

@@ -808,6 +808,12 @@ hipError_t G2V_CAT(launch_sgns_atomic_k, G2V_K)(const SgnsArgs& a, int nv, int g
   }
 #endif
 #endif
+#if G2V_K == 15 && defined(G2V_ABLATIONS)
+  if (nv == 2 && a.debug_write == 10) {  // the lost-update probe at the C4 shape
+    hipLaunchKernelGGL((k_sgns_atomic<15, 2, 10>), dim3(grid), dim3(kSgnsThreads), 0, st, a);
+    return hipGetLastError();
+  }
+#endif
   if (a.compute_loss) {
     if (nv == 1)
       hipLaunchKernelGGL((k_sgns_atomic<G2V_K, 1, 0, true>), dim3(grid), dim3(kSgnsThreads), 0, st,

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--pairs", type=int, default=20_000_000)
     ap.add_argument("--vocab", type=int, default=24447)
     ap.add_argument("--sample", type=float, default=1e-3)
+    ap.add_argument("--dim", type=int, default=200)
+    ap.add_argument("--negative", type=int, default=5)
     ap.add_argument("--epochs", type=int, default=2)
     ap.add_argument("--tails", default="auto,8192,4096,2048")
     ap.add_argument("--out", default=None)
@@ -42,7 +44,7 @@ def main():
     from gene2vec_amd import engine as E
     from gene2vec_amd import synthetic as S
 
-    D, K = 200, 5
+    D, K = a.dim, a.negative
     pairs = S.zipf_gene_pairs(a.pairs, a.vocab, 1.0, seed=20250114)
     flat = pairs.reshape(-1)
     counts, first = E.count_ids(flat, a.vocab)
@@ -74,8 +76,8 @@ def main():
             stores, changed = int(buf[14]), int(buf[15])
             per_epoch.append({"stores": stores, "lost": changed,
                               "lost_rate": changed / max(1, stores),
-                              "row_updates": 7 * st["examples"],
-                              "stored_share": stores / max(1, 7 * st["examples"]),
+                              "row_updates": (K + 2) * st["examples"],
+                              "stored_share": stores / max(1, (K + 2) * st["examples"]),
                               "tail_row_syn0": st["tail_row_syn0"],
                               "tail_row_syn1neg": st["tail_row_syn1neg"]})
             print(arm, ep, per_epoch[-1], flush=True)
