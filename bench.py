@@ -119,6 +119,9 @@ def parse():
     p.add_argument("--traffic-json", default=None,
                    help="PMC bytes per example for roofline.traffic (default: the newest "
                         "profiles/**/traffic_r*.json of this workload measured on this kernel build)")
+    p.add_argument("--library", default=None,
+                   help="A/B hook: load this libg2v build (gene2vec_amd.build.build(tag=...)) "
+                        "instead of gene2vec_amd/libg2v.so")
     p.add_argument("--launch-probe", action="store_true",
                    help="test hook: the ranks agree on the world over gloo and rank 0 prints "
                         "{n_gpus, ranks} without touching a GPU (checks --gpus N's own launcher)")
@@ -213,6 +216,8 @@ def main():
     import torch.distributed as dist
 
     from gene2vec_amd import _native as N
+    if a.library:
+        N.use_library(a.library)
     from gene2vec_amd import distributed as Dd
     from gene2vec_amd import engine as E
     from gene2vec_amd import synthetic as S
@@ -378,7 +383,8 @@ def main():
     # stamped with the hash of the kernel's sources), scaled to this run's
     # examples per launch; a profile of another build is refused (traffic null)
     from gene2vec_amd.build import kernel_source_hash
-    ksha = kernel_source_hash()
+    # (an A/B run of another build matches no traffic profile)
+    ksha = kernel_source_hash() if not a.library else "library " + os.path.basename(a.library)
     # the layout the timed launches actually used (g2v_stats): the grid and
     # stripe tiers are set_vocab's; the stability cap only holds waves back
     # inside a launch (waves_last_launch below)

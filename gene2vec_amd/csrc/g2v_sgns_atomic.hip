@@ -37,8 +37,11 @@ namespace g2v {
 // extra copies at once for D <= 256 (one memory latency per row instead of
 // three; round 5, interleaved A/B: C2 +0.9 %, sample 0 +0.5-1.6 %; round 2's
 // kernel had measured no difference), 7 at D > 256 (twice the registers)
+#ifndef G2V_STRIPE_BATCH1
+#define G2V_STRIPE_BATCH1 15  // (experiment builds override it)
+#endif
 template <int NV>
-constexpr int stripe_batch() { return NV == 1 ? 15 : 7; }
+constexpr int stripe_batch() { return NV == 1 ? G2V_STRIPE_BATCH1 : 7; }
 constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
 
 template <int K, int NV>
