@@ -1206,7 +1206,9 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
   if (atomic_kernel && (c->debug_write == 0 || c->debug_write == 8 || c->debug_write == 10) &&
       c->tail_store != 0) {
     int t0 = c->tail_store, t1 = c->tail_store;
-    if (c->tail_store < 0) {
+    if (c->tail_store < 0 && c->active_waves < kSgnsThreads / 64) {
+      t0 = t1 = c->V;  // auto is off in the one-wave parity mode (G2V_OPT_ACTIVE_WAVES)
+    } else if (c->tail_store < 0) {
       // auto: the collision budget over the waves this launch may run
       // (u(r), p_tok(r) are non-increasing in r: counts are sorted)
       const double waves = (double)launch_grid(c) * c->active_waves;

@@ -190,8 +190,11 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         (waves x the row's updates per example <= 0.15,
  *                         from the vocabulary of g2v_set_vocab; none at <=
  *                         ~5,000 genes), syn0 (the exported vectors) all
- *                         atomic; n > 0 = rows >= n of both tables, 0 = off;
- *                         g2v_stats reports the rows a launch used [-1]
+ *                         atomic; off with fewer than 4 active waves (the
+ *                         deterministic parity mode keeps its restated
+ *                         all-atomic order); n > 0 = rows >= n of both
+ *                         tables, 0 = off; g2v_stats reports the rows a
+ *                         launch used [-1]
  *   (keys 19 and 20, G2V_OPT_ATOMIC_TAILS / G2V_OPT_COPY_DEFER of ABI 4, were
  *    retired in ABI 5: both measured slower; G2V_EINVAL)
  *   G2V_OPT_DEBUG_FAIL_MERGE fault injection (tests of the failure paths): the
