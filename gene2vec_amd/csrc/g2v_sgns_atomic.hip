@@ -288,6 +288,28 @@ __device__ __forceinline__ void store_row(float* row, bool live, int D, const fl
                                           Pol<kPolWt>::st);
 }
 
+// The same store as 16-B lanes: the row's nvec float4 columns (element 4 c ..
+// 4 c + 3 in lane c mod 64 of vector c / 64), NV b128 instructions instead of
+// 4 NV b32 ones, plus 3 NV stores through an empty resource that the range
+// check drops whole (nothing reaches memory), so both sides of the store-or-
+// atomics if / else still count 4 NV vector-memory instructions for the loop
+// head's vmcnt.  The columns past D inside the last float4 are the tables'
+// zero padding, which every float4 kernel (loads, merges) already carries.
+#ifndef G2V_STORE_X4
+#define G2V_STORE_X4 1
+#endif
+template <int NV>
+__device__ __forceinline__ void store_row4(float* row, bool live, int nvec,
+                                           const float4 (&val)[NV], int lane) {
+  const __amdgpu_buffer_rsrc_t r = row_rsrc(row, live, 4 * nvec);
+  const __amdgpu_buffer_rsrc_t rz = row_rsrc(row, false, 0);
+#pragma unroll
+  for (int v = 0; v < NV; ++v) bstore4<Pol<kPolWt>::st>(r, (lane + 64 * v) * 16, val[v]);
+#pragma unroll
+  for (int i = 0; i < 3 * NV; ++i)  // distinct offsets, or they merge as dead stores
+    __builtin_amdgcn_raw_buffer_store_b32(0u, rz, (64 * i + lane) * 4, 0, 0);
+}
+
 #ifdef G2V_ABLATIONS
 // WR 10 (ablation build): before a cold row's store, re-read its first 64
 // floats write-through-fresh (sc1: past this CU's L1) and compare them with
@@ -714,13 +736,21 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         float* row = upd_row<WR>(a, 1, live[d] ? tg[d] : 0, cbase + d, rowb);
         const bool st = uniform_b(TS && slot[d] >= 0);
         if (st) {
-          float val[4 * NV];
-#pragma unroll
-          for (int i = 0; i < 4 * NV; ++i) val[i] = stl[slot[d] * 256 * NV + 64 * i + lane];
 #ifdef G2V_ABLATIONS
           if (WR == 10 && live[d]) lost_probe(row, s_to[wid][slot[d] * 64 + lane], a.stamps, lane);
 #endif
+#if G2V_STORE_X4
+          float4 val[NV];
+#pragma unroll
+          for (int v = 0; v < NV; ++v)
+            val[v] = *reinterpret_cast<const float4*>(stl + slot[d] * 256 * NV + (lane + 64 * v) * 4);
+          store_row4<NV>(row, live[d], a.nvec, val, lane);
+#else
+          float val[4 * NV];
+#pragma unroll
+          for (int i = 0; i < 4 * NV; ++i) val[i] = stl[slot[d] * 256 * NV + 64 * i + lane];
           store_row<NV>(row, live[d], D, val, lane);
+#endif
         } else {
           emit_row<NV, WR>(row, live[d], D, v1, g[d], lane);
         }
@@ -730,13 +760,25 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
         float* row = upd_row<WR>(a, 0, input, cbase + NT, rowb);
         const bool st = uniform_b(TS && input >= tail0);
         if (st) {
-          float val[4 * NV];
-#pragma unroll
-          for (int i = 0; i < 4 * NV; ++i) val[i] = __fmaf_rn(lf, vw[i], v1[i]);
 #ifdef G2V_ABLATIONS
           if (WR == 10 && any) lost_probe(row, v1[0], a.stamps, lane);
 #endif
+#if G2V_STORE_X4
+          float4 val[NV];
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+            const float4 l = *reinterpret_cast<const float4*>(s1 + (lane + 64 * v) * 4);
+            const float4 w = *reinterpret_cast<const float4*>(sw + (lane + 64 * v) * 4);
+            val[v] = make_float4(__fmaf_rn(lf, w.x, l.x), __fmaf_rn(lf, w.y, l.y),
+                                 __fmaf_rn(lf, w.z, l.z), __fmaf_rn(lf, w.w, l.w));
+          }
+          store_row4<NV>(row, any, a.nvec, val, lane);
+#else
+          float val[4 * NV];
+#pragma unroll
+          for (int i = 0; i < 4 * NV; ++i) val[i] = __fmaf_rn(lf, vw[i], v1[i]);
           store_row<NV>(row, any, D, val, lane);
+#endif
         } else {
           emit_row<NV, WR>(row, any && WR != 5, D, vw, lf, lane);
         }
