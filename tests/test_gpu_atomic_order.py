@@ -129,14 +129,15 @@ def _no_consecutive_share(V, K, n, seed, zipf=True):
     return c, i, negs
 
 
-@pytest.mark.parametrize("tail,D,K", [(100, 200, 5), (1, 200, 5), (1, 512, 15)])
+@pytest.mark.parametrize("tail,D,K", [(100, 200, 5), (1, 200, 5), (1, 512, 15), (1, 37, 3)])
 def test_one_wave_tail_stores_match_restatement(tail, D, K):
     """G2V_OPT_TAIL_STORE: on one wave, with no row shared by
     consecutive examples, a cold row's plain store of (row as read + delta)
     leaves the same value as the atomic (row + delta): the kernel still
     matches orc_atomic_one_wave at 1e-5, repeated targets (atomics) included;
     tail 1 = every unstriped row stored (at negative 15 more cold rows than
-    the 8 staging slots: the rest take atomics)"""
+    the 8 staging slots: the rest take atomics; at D 37 the 16-B stores also
+    write the last float4's zero padding, which must stay zero)"""
     V, n, alpha = (2000, 1500, 0.025) if K == 5 else (6000, 800, 0.025)
     rng = np.random.RandomState(3)
     syn0 = ((rng.rand(V, D) - 0.5) / D).astype(np.float32)
