@@ -18,7 +18,7 @@ namespace g2v {
 // read-modify-write stores lose most updates (measured: iteration-0 loss 4.15
 // vs 2.77 sequential); atomics keep all of them (2.76).
 //
-// Pipelining: a wave takes chunks of kChunk consecutive
+// Pipelining: a wave takes chunks of kAChunk consecutive
 // examples from a work queue and stages each chunk's records and lockf in LDS
 // once.  Example e+1's rows are loaded BEFORE example e's atomics are issued
 // and after example e-1's have landed (the wave sees its own updates from two
@@ -42,7 +42,14 @@ namespace g2v {
 #endif
 template <int NV>
 constexpr int stripe_batch() { return NV == 1 ? G2V_STRIPE_BATCH1 : 7; }
-constexpr int kStripeOob = (int)kStripeMaxBytes;  // past any stripe buffer (run_sgns clamps rows)
+constexpr int kStripeOob = (int)kStripeMaxBytes;
+// examples per work-queue chunk of k_sgns_atomic (<= 64: one lockf per lane
+// when the chunk is staged); oracle/c_oracle.py atomic_one_wave(chunk=) follows
+#ifndef G2V_CHUNK
+#define G2V_CHUNK 32  // (experiment builds override it)
+#endif
+constexpr int kAChunk = G2V_CHUNK;
+static_assert(kAChunk >= 1 && kAChunk <= 64, "one lockf per lane");  // past any stripe buffer (run_sgns clamps rows)
 
 template <int K, int NV>
 struct ExRegs {
@@ -332,7 +339,7 @@ __device__ __forceinline__ void lost_probe(float* row, float old, unsigned long 
 // LOSS ([ext] compute_loss): each wave keeps a float32 partial of the
 // -log(sigmoid(+-f)) LOG_TABLE terms over its chunk and adds it to a double
 // accumulator once per chunk; LOSS = false compiles the tally out.
-// Chunks of kChunk consecutive examples are handed out by a work queue (one
+// Chunks of kAChunk consecutive examples are handed out by a work queue (one
 // counter, lane 0's returning atomic): every wave works near the front of
 // the record stream whatever its speed.  With a static grid-stride split,
 // waves that share a CU (grid not a multiple of the CU count) fall behind
@@ -397,8 +404,8 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
   __shared__ float s_wk[W][256 * NV];
   __shared__ float s_tl[W][TS ? kSlots * 256 * NV : 1];  // tail rows' new values (TS)
   __shared__ float s_to[W][WR == 10 ? kSlots * 64 : 1];  // WR 10: their old first 64 floats
-  __shared__ int32_t s_rec[W][kChunk * RS];  // the wave's chunk of records
-  __shared__ float s_lf[W][kChunk];          // lockf[input] per record of the chunk
+  __shared__ int32_t s_rec[W][kAChunk * RS];  // the wave's chunk of records
+  __shared__ float s_lf[W][kAChunk];          // lockf[input] per record of the chunk
   for (int i = threadIdx.x; i < kExpTableSize; i += kSgnsThreads) {
     s_lut[i] = a.exp_table[i];
     if (LOSS) s_log[i] = a.log_table[i];
@@ -463,9 +470,9 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
     rl0 = stamp_realtime();
     tl0 = stamp_time();
   }
-  for (int64_t c = next_chunk(a.queue, lane); c * kChunk < E; c = next_chunk(a.queue, lane)) {
-    const int64_t e_beg = c * kChunk;
-    const int64_t e_end = (e_beg + kChunk < E) ? e_beg + kChunk : E;
+  for (int64_t c = next_chunk(a.queue, lane); c * kAChunk < E; c = next_chunk(a.queue, lane)) {
+    const int64_t e_beg = c * kAChunk;
+    const int64_t e_end = (e_beg + kAChunk < E) ? e_beg + kAChunk : E;
     // stage the chunk's records and their lockf once: per example, only row
     // loads and atomics are vector-memory operations
     {
