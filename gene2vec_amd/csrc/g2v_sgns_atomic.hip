@@ -278,9 +278,10 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 // G2V_OPT_TAIL_STORE: a cold row (syn0 index >= a.tail_row0,
 // syn1neg index >= a.tail_row1, never a striped row; syn1neg rows only in a
 // repeat-free example) is written with plain stores of its new value, the
-// element-order row val[0, 4 NV), instead of float atomics of the delta: the
-// same 4 NV wave-instructions of 256 contiguous bytes, write-through (sc1: the
-// line leaves the writer's L2, so a later read on that XCD fetches the memory
+// element-order row val[0, 4 NV), instead of float atomics of the delta: 4 NV
+// wave-instructions of 256 contiguous bytes (this form, G2V_STORE_X4=0) or NV
+// of 16-B lanes (store_row4 below, the default), write-through (sc1: the line
+// leaves the writer's L2, so a later read on that XCD fetches the memory
 // side's copy).  gensim's own Hogwild read-modify-write, with the lost updates
 // that implies when another wave wrote the row between this wave's read and
 // its store -- which is why only rows that other in-flight waves rarely touch
@@ -729,8 +730,9 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
       }
 #endif
       // syn1neg[tg[d]] += g[d] * l1 (d = 0..K), then syn0[input] += lockf * work;
-      // a cold row (G2V_OPT_TAIL_STORE) takes its 4 NV stores INSTEAD: a
-      // uniform if / else with 4 NV vector-memory instructions on each side,
+      // a cold row (G2V_OPT_TAIL_STORE) takes its stores INSTEAD: a uniform
+      // if / else with 4 NV vector-memory instructions on each side (store_row4
+      // pads its NV 16-B stores with dropped ones),
       // so the loop head waits for the next example's loads with
       // vmcnt(#row instructions).  That needs the build's
       // -structurizecfg-skip-uniform-regions (gene2vec_amd/build.py): the
