@@ -64,9 +64,13 @@ def main():
     ap.add_argument("--engines", default="gpu,oracle",
                     help="gpu (libg2v Hogwild), gpu_seq (libg2v sequential mode), gpu_gridN "
                          "(Hogwild on N workgroups), gpu_uncapped (Hogwild fixed at set_vocab's "
-                         "default grid: no per-call stability cap), oracle (sequential), "
+                         "default grid: no per-call stability cap), gpu_tailN (Hogwild with "
+                         "G2V_OPT_TAIL_STORE N: gpu_tail0 every row atomic; gpu = the default, "
+                         "the collision budget), oracle (sequential), "
                          "oracle_hogN (the C restatement's OpenMP Hogwild on N threads: gensim "
                          "workers=N)")
+    ap.add_argument("--reference-engine", default="oracle",
+                    help="the engine the summary's gaps are taken against (oracle, oracle_hogN)")
     ap.add_argument("--per-iter", action="store_true", help="print the GPU runs' objective per iteration")
     ap.add_argument("--out", default="gpurun_out/e2e_parity")
     a = ap.parse_args()
@@ -124,8 +128,10 @@ def main():
     p_tok_max = float((pt / pt.sum()).max())
     log["config"]["p_tok_max"] = p_tok_max
 
-    def train_gpu(seed, mode=N.MODE_HOGWILD, grid=0, overlap=None):
+    def train_gpu(seed, mode=N.MODE_HOGWILD, grid=0, overlap=None, tail=None):
         eng = E.SGNSEngine(V, D, K)
+        if tail is not None:
+            eng.set_option(N.OPT_TAIL_STORE, tail)
         if grid == -1:  # set_vocab's default, fixed (no per-call cap)
             probe = E.SGNSEngine(V, D, K)
             probe.set_vocab(vc, a.sample)
@@ -158,7 +164,9 @@ def main():
                       f"{n0.max():.2f}/{n0[:20].max():.2f} |syn1neg|^2 max/top20 "
                       f"{n1.max():.2f}/{n1[:20].max():.2f}", flush=True)
         st = eng.read_stats()
-        extra = {"grid": int(eng.get_option(N.OPT_GRID)), "last_launch_waves": int(st["sgns_waves"])}
+        extra = {"grid": int(eng.get_option(N.OPT_GRID)), "last_launch_waves": int(st["sgns_waves"]),
+                 "tail_row_syn1neg": int(st["tail_row_syn1neg"]),
+                 "tail_row_syn0": int(st["tail_row_syn0"])}
         s0, s1 = eng.get_weights()
         eng.close()
         return s0, s1, {"loss": float(st["training_loss"]), **extra}
@@ -190,6 +198,8 @@ def main():
                 s0, s1, extra = train_gpu(seed, overlap=int(eng_name[6:]))
             elif eng_name.startswith("gpu_grid"):
                 s0, s1, extra = train_gpu(seed, grid=int(eng_name[8:]))
+            elif eng_name.startswith("gpu_tail"):
+                s0, s1, extra = train_gpu(seed, tail=int(eng_name[8:]))
             elif eng_name == "gpu_uncapped":
                 s0, s1, extra = train_gpu(seed, grid=-1)
             elif eng_name.startswith("oracle_hog"):
@@ -215,13 +225,22 @@ def main():
         v = [r[key] for t, r in log["runs"].items() if t.startswith(engine + "_seed") and key in r]
         return float(np.mean(v)) if v else None
     summ = {}
+    ref = a.reference_engine
+    others = [x for x in a.engines.split(",") if x != ref]
+    summ["reference"] = ref
     for key in ("loss", "heldin", "target_ratio", "auc_mean"):
-        g, o = mean("gpu", key), mean("oracle", key)
-        ov = [r[key] for t, r in log["runs"].items() if t.startswith("oracle_seed") and key in r]
-        summ[key] = {"gpu": g, "oracle": o,
-                     "gap": None if g is None or o is None else round((g - o) / o, 5),
+        o = mean(ref, key)
+        ov = [r[key] for t, r in log["runs"].items() if t.startswith(ref + "_seed") and key in r]
+        summ[key] = {"oracle": o,
                      "oracle_spread": round((max(ov) - min(ov)) / abs(np.mean(ov)), 5)
                      if len(ov) > 1 else None}
+        for eng_name in others:
+            g = mean(eng_name, key)
+            summ[key][eng_name] = g
+            summ[key][eng_name + "_gap"] = (None if g is None or o is None
+                                            else round((g - o) / o, 5))
+        if "gpu" in others:  # (the field name earlier rounds' files use)
+            summ[key]["gap"] = summ[key]["gpu_gap"]
     log["summary"] = summ
     json.dump(log, open(os.path.join(a.out, "e2e_parity.json"), "w"), indent=1)
     print(json.dumps(summ, indent=1))
