@@ -277,35 +277,22 @@ __device__ __forceinline__ void emit_row(float* row, bool live, int D, const flo
 
 // G2V_OPT_TAIL_STORE: a cold row (syn0 index >= a.tail_row0,
 // syn1neg index >= a.tail_row1, never a striped row; syn1neg rows only in a
-// repeat-free example) is written with plain stores of its new value, the
-// element-order row val[0, 4 NV), instead of float atomics of the delta: 4 NV
-// wave-instructions of 256 contiguous bytes (this form, G2V_STORE_X4=0) or NV
-// of 16-B lanes (store_row4 below, the default), write-through (sc1: the line
-// leaves the writer's L2, so a later read on that XCD fetches the memory
-// side's copy).  gensim's own Hogwild read-modify-write, with the lost updates
-// that implies when another wave wrote the row between this wave's read and
-// its store -- which is why only rows that other in-flight waves rarely touch
-// take it (run_sgns's collision budget).
-template <int NV>
-__device__ __forceinline__ void store_row(float* row, bool live, int D, const float (&val)[4 * NV],
-                                          int lane) {
-  const __amdgpu_buffer_rsrc_t r = row_rsrc(row, live, D);
-#pragma unroll
-  for (int i = 0; i < 4 * NV; ++i)
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(val[i]), r, (64 * i + lane) * 4, 0,
-                                          Pol<kPolWt>::st);
-}
-
-// The same store as 16-B lanes: the row's nvec float4 columns (element 4 c ..
-// 4 c + 3 in lane c mod 64 of vector c / 64), NV b128 instructions instead of
-// 4 NV b32 ones, plus 3 NV stores through an empty resource that the range
-// check drops whole (nothing reaches memory), so both sides of the store-or-
-// atomics if / else still count 4 NV vector-memory instructions for the loop
-// head's vmcnt.  The columns past D inside the last float4 are the tables'
-// zero padding, which every float4 kernel (loads, merges) already carries.
-#ifndef G2V_STORE_X4
-#define G2V_STORE_X4 1
-#endif
+// repeat-free example) is written with plain stores of its new value instead
+// of float atomics of the delta, write-through (sc1: the line leaves the
+// writer's L2, so a later read on that XCD fetches the memory side's copy).
+// gensim's own Hogwild read-modify-write, with the lost updates that implies
+// when another wave wrote the row between this wave's read and its store --
+// which is why only rows that other in-flight waves rarely touch take it
+// (run_sgns's collision budget).
+//
+// The row leaves as 16-B lanes: its nvec float4 columns (element 4 c .. 4 c + 3
+// in lane c mod 64 of vector c / 64), NV b128 instructions, plus 3 NV stores
+// through an empty resource that the range check drops whole (nothing reaches
+// memory), so both sides of the store-or-atomics if / else count 4 NV
+// vector-memory instructions for the loop head's vmcnt.  (Round 5 A/B against
+// 4 NV b32 stores: C4 +1.3 %, C2 equal; the b32 form was removed.)  The columns
+// past D inside the last float4 are the tables' zero padding, which every
+// float4 kernel (loads, merges) already carries.
 template <int NV>
 __device__ __forceinline__ void store_row4(float* row, bool live, int nvec,
                                            const float4 (&val)[NV], int lane) {
@@ -578,7 +565,7 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
             work[v].w = __fmaf_rn(gg, x.rw[d][v].w, work[v].w);
           }
           if (TS && x.tg[d] >= tail1 && nslot < kSlots) {
-            // the cold row's new value, staged in element order for store_row
+            // the cold row's new value, staged in element order for store_row4
             if (WR == 10 && lane < 16)
               *reinterpret_cast<float4*>(s_to[wid] + nslot * 64 + lane * 4) = x.rw[d][0];
 #pragma unroll
@@ -748,18 +735,11 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #ifdef G2V_ABLATIONS
           if (WR == 10 && live[d]) lost_probe(row, s_to[wid][slot[d] * 64 + lane], a.stamps, lane);
 #endif
-#if G2V_STORE_X4
           float4 val[NV];
 #pragma unroll
           for (int v = 0; v < NV; ++v)
             val[v] = *reinterpret_cast<const float4*>(stl + slot[d] * 256 * NV + (lane + 64 * v) * 4);
           store_row4<NV>(row, live[d], a.nvec, val, lane);
-#else
-          float val[4 * NV];
-#pragma unroll
-          for (int i = 0; i < 4 * NV; ++i) val[i] = stl[slot[d] * 256 * NV + 64 * i + lane];
-          store_row<NV>(row, live[d], D, val, lane);
-#endif
         } else {
           emit_row<NV, WR>(row, live[d], D, v1, g[d], lane);
         }
@@ -772,7 +752,6 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
 #ifdef G2V_ABLATIONS
           if (WR == 10 && any) lost_probe(row, v1[0], a.stamps, lane);
 #endif
-#if G2V_STORE_X4
           float4 val[NV];
 #pragma unroll
           for (int v = 0; v < NV; ++v) {
@@ -782,12 +761,6 @@ __global__ __launch_bounds__(kSgnsThreads) void k_sgns_atomic(SgnsArgs a) {
                                  __fmaf_rn(lf, w.z, l.z), __fmaf_rn(lf, w.w, l.w));
           }
           store_row4<NV>(row, any, a.nvec, val, lane);
-#else
-          float val[4 * NV];
-#pragma unroll
-          for (int i = 0; i < 4 * NV; ++i) val[i] = __fmaf_rn(lf, vw[i], v1[i]);
-          store_row<NV>(row, any, D, val, lane);
-#endif
         } else {
           emit_row<NV, WR>(row, any && WR != 5, D, vw, lf, lane);
         }
