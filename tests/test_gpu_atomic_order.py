@@ -137,16 +137,18 @@ def test_one_wave_tail_stores_match_restatement(tail, D, K):
     matches orc_atomic_one_wave at 1e-5, repeated targets (atomics) included;
     tail 1 = every unstriped row stored (at negative 15 more cold rows than
     the 8 staging slots: the rest take atomics; at D 37 the 16-B stores also
-    write the last float4's zero padding, which must stay zero)"""
+    write the last float4's zero padding, which must stay zero); syn0_lockf
+    0 / 0.5 / 1 per row"""
     V, n, alpha = (2000, 1500, 0.025) if K == 5 else (6000, 800, 0.025)
     rng = np.random.RandomState(3)
     syn0 = ((rng.rand(V, D) - 0.5) / D).astype(np.float32)
     syn1 = ((rng.rand(V, D) - 0.5) / D * 0.1).astype(np.float32)
-    lockf = np.ones(V, np.float32)
+    # locked, half-locked and free syn0 rows: a stored syn0 row is l1 + lockf * work
+    lockf = np.random.RandomState(7).choice([0.0, 0.5, 1.0], V).astype(np.float32)
     c, i, negs = _no_consecutive_share(V, K, n, seed=tail + K, zipf=K == 5)
     negs[5::97, 1] = negs[5::97, 0]  # some repeated targets: those examples keep atomics
     e = E.SGNSEngine(V, D, K)
-    e.set_weights(syn0, syn1)
+    e.set_weights(syn0, syn1, lockf)
     e.set_option(N.OPT_GRID, 1)
     e.set_option(N.OPT_ACTIVE_WAVES, 1)
     for k, v in STRIPES["two_tier"].items():
