@@ -186,6 +186,14 @@ class HostCollective:
 
 
 def host_collective(group=None):
+    """HostCollective over `group`; without one, over the default group when
+    that is gloo, else over a new gloo group of every rank (its CPU tensors
+    cannot go through an nccl default group: `--merge-transport host` on a
+    GPU node).  Collective: every rank calls it at the same point."""
+    if group is None:
+        import torch.distributed as dist
+        if dist.is_initialized() and dist.get_backend() != "gloo":
+            group = dist.new_group(backend="gloo")
     return HostCollective(group)
 
 
