@@ -65,6 +65,40 @@ def usable_cpus():
     return min(host, aff, quota or host), host, aff, quota
 
 
+def stored_rows_per_example(vcounts, sample, K, tail_row_syn0, tail_row_syn1neg):
+    """Expected rows per directed example that leave as plain stores
+    (G2V_OPT_TAIL_STORE): syn1neg rows from tail_row_syn1neg on
+    (the centre with its kept-token share p_tok, the K negatives with the
+    unigram^0.75 share p_neg), the syn0 input row from tail_row_syn0 on (p_tok);
+    -1 = none.  An expectation over the vocabulary: the kernel also keeps
+    atomics for examples with a repeated target, so the lost-update probe's
+    exact store count runs ~0.6 % lower at C2 (1.476 vs 1.485 rows)."""
+    from gene2vec_amd import engine as E
+    vc = np.asarray(vcounts)
+    pt = E.kept_token_share(vc, sample)
+    pn = vc.astype(np.float64) ** 0.75
+    pn /= pn.sum()
+    rows = 0.0
+    if tail_row_syn1neg >= 0:
+        rows += pt[tail_row_syn1neg:].sum() + K * pn[tail_row_syn1neg:].sum()
+    if tail_row_syn0 >= 0:
+        rows += pt[tail_row_syn0:].sum()
+    return float(rows)
+
+
+def composite_roofline(update_bytes, stored_bytes, s_per_example,
+                       atomic_peak=ATOMIC_PEAK_GBPS, store_peak=STORE_PEAK_GBPS):
+    """(achieved, peak, frac) in GB/s of update bytes for k_sgns_atomic: the
+    atomic bytes leave at the memory-side float-atomic rate, the stored bytes
+    at the plain-store rate, so the roof time per example is atomic /
+    atomic_peak + stored / store_peak and peak = update bytes / that time"""
+    atomic_bytes = update_bytes - stored_bytes
+    roof_s = atomic_bytes / (atomic_peak * 1e9) + stored_bytes / (store_peak * 1e9)
+    peak = update_bytes / roof_s / 1e9
+    achieved = update_bytes / s_per_example / 1e9 if s_per_example > 0 else 0.0
+    return achieved, peak, achieved / peak
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -437,20 +471,14 @@ def main():
     # The HBM view of the same launches (2*(K+2)*D*4 bytes per example: every
     # updated row read and written) stays beside it as hbm_*.
     update_bytes = (K + 2) * D * 4
-    pt_r = E.kept_token_share(vcounts, a.sample)
-    pn_r = vcounts.astype(np.float64) ** 0.75
-    pn_r /= pn_r.sum()
     t0r, t1r = st["tail_row_syn0"], st["tail_row_syn1neg"]
-    stored_rows = ((pt_r[t1r:].sum() + K * pn_r[t1r:].sum()) if t1r >= 0 else 0.0) \
-        + (pt_r[t0r:].sum() if t0r >= 0 else 0.0)
+    stored_rows = stored_rows_per_example(vcounts, a.sample, K, t0r, t1r)
     stored_bytes = stored_rows * D * 4
     atomic_bytes = update_bytes - stored_bytes
     t_ex = st["sgns_kernel_ms"] / 1e3 / max(1, st["examples"])  # s per example
-    roof_t_ex = atomic_bytes / (ATOMIC_PEAK_GBPS * 1e9) + stored_bytes / (STORE_PEAK_GBPS * 1e9)
-    upd_gbps = update_bytes / t_ex / 1e9 if t_ex > 0 else 0.0
-    peak_gbps = update_bytes / roof_t_ex / 1e9
+    upd_gbps, peak_gbps, frac = composite_roofline(update_bytes, stored_bytes, t_ex)
     roofline = {"bound": "atomics", "achieved": round(upd_gbps, 1), "peak": round(peak_gbps, 1),
-                "unit": "GB/s", "frac": round(upd_gbps / peak_gbps, 4),
+                "unit": "GB/s", "frac": round(frac, 4),
                 "traffic": traffic,
                 "kernel": "k_sgns_atomic", "avg_launch_ms": round(avg_launch_ms, 4),
                 "update_bytes_per_example": update_bytes,
