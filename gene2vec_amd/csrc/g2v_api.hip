@@ -308,16 +308,19 @@ constexpr double kTailCollision = 0.15;
 // read of a striped row sums its copies (one more load batch on the example's
 // critical path); every copy spreads that row's atomics.  At one workgroup per
 // CU or more the kernel is bound by the memory-side atomics and 16 copies win
-// (C2 266 WGs: 202.6 M ex/s vs 197.2 with 8); below, the grid is held down by
-// the staleness budget, per-example latency binds and 8 win (C2 sample 0 at
-// 162 WGs: 153.6 vs 136.4; C4 at 121: 36.8 vs 36.1).
+// (C2 266 WGs: 202.6 M ex/s vs 197.2 with 8).  Below, the grid is held down by
+// the staleness budget and per-example latency binds: at D <= 256 the kernel
+// loads all 15 extra copies in one batch (stripe_batch<1>, round 5), so 16
+// copies cost no more latency than 8 and still spread the atomics (C2 sample 0
+// at 162 WGs, round 5: 61.7 / 61.7 ms per launch vs 63.2 / 65.5 with 8); at
+// D > 256 (batches of 7) 8 win (C4 at 121: 36.8 vs 36.1).
 // the Hogwild grid of the launches being issued (the stability cap, DESIGN.md
 // 5c, lowers the waves that train inside a launch, not the grid)
 static int launch_grid(const g2v_ctx* c) { return c->sgns_grid; }
 
 static int stripe_copies_eff(const g2v_ctx* c) {
   if (c->stripe_copies > 0) return c->stripe_copies;
-  return launch_grid(c) >= c->cus ? 16 : 8;
+  return (launch_grid(c) >= c->cus || c->nv == 1) ? 16 : 8;
 }
 
 // Second stripe tier when G2V_OPT_STRIPE2_ROWS is not set: rows 8..19 get 4

@@ -150,8 +150,9 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         -1 = auto: 20 when the SGNS grid fills every CU,
  *                         else off [-1]
  *   G2V_OPT_STRIPE2_COPIES copies per second-tier row: 2, 4 or 8 [4]
- *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off, 0 = auto: 16 when the
- *                         SGNS grid fills every CU, 8 below [0] (values stay
+ *   G2V_OPT_STRIPE_COPIES copies per striped row, 1 = off, 0 = auto: 16 at
+ *                         vector_size <= 256 or when the SGNS grid fills every
+ *                         CU, 8 otherwise [0] (values stay
  *                         exact: readers sum the copies, each launch folds them
  *                         back; g2v_get_option reads the value in use)
  *   G2V_OPT_ATOMIC_OVERLAP Hogwild kernel: 1 = a wave's table atomics retire
