@@ -142,7 +142,10 @@ struct g2v_ctx {
   int hot_rows = -1;            // -1: default (all rows atomic-updated); tuned via g2v_set_option
   int cache_policy = 1;         // kPolWt
   int debug_write = 0;
-  int stripe_rows = 8, stripe_copies = 0;  // copies 0 = auto (stripe_copies_eff)
+  // 4 hottest rows striped (round 5, interleaved A/B against 8 with the 16-copy
+  // default: sample 0 +1.5-2.6 %, C4 +1.8 %, C2 +0.1-0.5 %, a 3,000-gene corpus
+  // within its noise; 2 rows lose 10 % at sample 0)
+  int stripe_rows = 4, stripe_copies = 0;  // copies 0 = auto (stripe_copies_eff)
   int stripe2_rows = -1, stripe2_copies = 4;  // second tier: rows [stripe_rows, stripe2_rows), -1 = auto
   float* stripe2 = nullptr;
   int64_t stripe2_cap = 0;
@@ -323,7 +326,7 @@ static int stripe_copies_eff(const g2v_ctx* c) {
   return (launch_grid(c) >= c->cus || c->nv == 1) ? 16 : 8;
 }
 
-// Second stripe tier when G2V_OPT_STRIPE2_ROWS is not set: rows 8..19 get 4
+// Second stripe tier when G2V_OPT_STRIPE2_ROWS is not set: rows up to 19 get 4
 // copies each when the grid fills every CU (C2, interleaved A/B: 203.6 vs
 // 200.3 M ex/s; 24 rows 203.0, 32 rows 202.0), none below, where per-example
 // latency binds and the extra copy reads cost (C2 sample 0 at 162 WGs: 153.5

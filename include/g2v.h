@@ -144,7 +144,7 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         wave had changed before the store landed); any
  *                         mode this library does not compile, or a shape it
  *                         is not compiled for, is G2V_EINVAL [0]
- *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [8]
+ *   G2V_OPT_STRIPE_ROWS   hottest rows of each table striped over copies [4]
  *   G2V_OPT_STRIPE2_ROWS  second stripe tier: rows [STRIPE_ROWS, this) get
  *                         STRIPE2_COPIES copies each (<= STRIPE_ROWS = off);
  *                         -1 = auto: 20 when the SGNS grid fills every CU,

@@ -23,8 +23,11 @@ pytestmark = pytest.mark.gpu
 
 STRIPES = {
     "off": {N.OPT_STRIPE_COPIES: 1},
-    "default": {},                     # one workgroup < CUs: 8 rows x 8 copies, no tier 2
-    "two_tier": {N.OPT_STRIPE_COPIES: 16, N.OPT_STRIPE2_ROWS: 20, N.OPT_STRIPE2_COPIES: 4},
+    # the library's default at one workgroup (< CUs): 4 rows x 16 copies at
+    # D <= 256, x 8 above, no tier 2
+    "default": {},
+    "two_tier": {N.OPT_STRIPE_ROWS: 8, N.OPT_STRIPE_COPIES: 16, N.OPT_STRIPE2_ROWS: 20,
+                 N.OPT_STRIPE2_COPIES: 4},
 }
 
 
@@ -66,6 +69,9 @@ def test_one_wave_atomic_kernel_matches_restatement(D, K, stripes):
     assert st["sgns_grid"] == 1
     if stripes == "off":
         assert st["stripe_copies"] == 1
+    if stripes == "default":
+        assert (st["stripe_rows"], st["stripe_copies"], st["stripe2_rows"]) == \
+            (4, 16 if D <= 256 else 8, 4)
     if stripes == "two_tier":
         assert (st["stripe_rows"], st["stripe_copies"], st["stripe2_rows"],
                 st["stripe2_copies"]) == (8, 16, 20, 4)
