@@ -33,12 +33,13 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # experiment hook: G2V_TEST_TAIL_STORE=n trains both arms with
 # G2V_OPT_TAIL_STORE n
-TAIL_STORE = int(os.environ.get("G2V_TEST_TAIL_STORE", "0"))
+_ts = os.environ.get("G2V_TEST_TAIL_STORE")  # unset: the library's default (-1, auto)
+TAIL_STORE = int(_ts) if _ts not in (None, "") else None
 
 
 def _opts():
     from gene2vec_amd import _native as N
-    return {N.OPT_TAIL_STORE: TAIL_STORE} if TAIL_STORE else {}
+    return {N.OPT_TAIL_STORE: TAIL_STORE} if TAIL_STORE is not None else {}
 
 
 def _progress():

@@ -34,7 +34,8 @@ from tests.helpers import E2E, E2E_C2, E2E_V5K, e2e_corpus, e2e_heldin
 pytestmark = pytest.mark.gpu
 # experiment hook (verdict r4 item 4): G2V_TEST_TAIL_STORE=n
 # runs these gates with G2V_OPT_TAIL_STORE n (cold rows stored, not added)
-TAIL_STORE = int(os.environ.get("G2V_TEST_TAIL_STORE", "0"))
+_ts = os.environ.get("G2V_TEST_TAIL_STORE")  # unset: the library's default (-1, auto)
+TAIL_STORE = int(_ts) if _ts not in (None, "") else None
 
 
 def _train_e2e(tmp_path, sample, grid=None, cfg=E2E):
@@ -52,7 +53,7 @@ def _train_e2e(tmp_path, sample, grid=None, cfg=E2E):
         eng = E.SGNSEngine(V, D, K)
         if grid:
             eng.set_option(N.OPT_GRID, grid)
-        if TAIL_STORE:
+        if TAIL_STORE is not None:
             eng.set_option(N.OPT_TAIL_STORE, min(TAIL_STORE, V))
         eng.set_vocab(counts, sample)
         eng.set_weights(syn0, np.zeros_like(syn0))
