@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 5: cold-row stores as 16-B lanes (1 b128 + 3 dropped pads per 1 KB) vs
-# (historical: the b32 arm was an experiment build with -DG2V_STORE_X4=0; that form was removed after this A/B)
 # 4 b32 stores per row (b32): parity of the tail-store order, then bench A/B
+# (historical: the b32 arm was an experiment build with -DG2V_STORE_X4=0; that form was removed after this A/B)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r05c24
