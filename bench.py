@@ -105,6 +105,12 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--pairs", type=int, default=0, help="pairs per GPU (0 = 100M at N=1, 125M at N>1)")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                   help="weak (default): --pairs per GPU; strong: --total-pairs split over the "
+                        "N GPUs (SURVEY 8(d) C3's 1 B / N curve; N = 1 trains all of them)")
+    p.add_argument("--total-pairs", type=int, default=1_000_000_000,
+                   help="--scaling strong: pairs of the whole job (each rank trains "
+                        "total / N, its own shard of the generator)")
     p.add_argument("--vocab", type=int, default=24447)
     p.add_argument("--dim", type=int, default=200)
     p.add_argument("--negative", type=int, default=5)
@@ -208,11 +214,24 @@ def launch_ranks(n):
     return rc
 
 
-def launch_probe(world, rank):
-    """--launch-probe: the N ranks of a spawned run meet over gloo (CPU only)"""
+def pairs_per_rank(a, world):
+    """pairs each rank trains per step: weak scaling --pairs (100 M at N = 1,
+    the C2 line; 125 M at N > 1, C3's 1 B over 8); strong scaling
+    --total-pairs / N"""
+    if a.scaling == "strong":
+        if a.pairs:
+            sys.exit("bench.py: --scaling strong takes --total-pairs, not --pairs")
+        return a.total_pairs // world
+    return a.pairs or (100_000_000 if world == 1 else 125_000_000)
+
+
+def launch_probe(a, world, rank):
+    """--launch-probe: the N ranks of a spawned run meet over gloo (CPU only)
+    and rank 0 reports the world and the shard each rank would train"""
+    shape = {"scaling": a.scaling, "pairs_per_rank": pairs_per_rank(a, world)}
     if world == 1:
-        print(json.dumps({"probe": True, "n_gpus": 1, "rank_sum": 1, "ranks_expected_sum": 1}),
-              flush=True)
+        print(json.dumps({"probe": True, "n_gpus": 1, "rank_sum": 1, "ranks_expected_sum": 1,
+                          **shape}), flush=True)
         return
     import torch
     import torch.distributed as dist
@@ -221,7 +240,7 @@ def launch_probe(world, rank):
     dist.all_reduce(t)
     if rank == 0:
         print(json.dumps({"probe": True, "n_gpus": world, "rank_sum": int(t.item()),
-                          "ranks_expected_sum": world * (world + 1) // 2}), flush=True)
+                          "ranks_expected_sum": world * (world + 1) // 2, **shape}), flush=True)
     dist.destroy_process_group()
 
 
@@ -239,7 +258,7 @@ def main():
     if a.gpus < 1:
         sys.exit("bench.py: --gpus must be >= 1")
     if a.launch_probe:
-        launch_probe(int(env_world or 1), int(os.environ.get("RANK", "0")))
+        launch_probe(a, int(env_world or 1), int(os.environ.get("RANK", "0")))
         return
     # stdout carries exactly one JSON line: the libraries' own chatter (RCCL
     # prints its version banner from C on fd 1) goes to stderr until then
@@ -275,7 +294,7 @@ def main():
         else:
             dist.init_process_group("gloo")
     dev = torch.device("cuda", local)
-    n_pairs = a.pairs or (100_000_000 if world == 1 else 125_000_000)
+    n_pairs = pairs_per_rank(a, world)
     V0, D, K = a.vocab, a.dim, a.negative
 
     # ---- corpus shard + global vocabulary ---------------------------------------
@@ -447,11 +466,15 @@ def main():
             continue
         traffic = round((tj["fetch_bytes_per_example"] + tj["write_bytes_per_example"])
                         * st["examples"] / launches, 1)
+        # the same profile's L2 hit rate and VALU busy (scripts/pmc_traffic.py)
+        counter_extras = {k: tj[k] for k in ("l2_hit_rate", "valu_busy", "valu_insts_per_cycle_per_simd",
+                                              "traffic_over_algorithmic") if k in tj}
         traffic_src = (f"{os.path.relpath(tpath, ROOT)} (kernel build {ksha}, same launch "
                        "layout): PMC bytes "
                        f"per example x this run's {st['examples'] // launches} examples per "
                        "launch (not measured in this process)")
     if traffic is None:
+        counter_extras = {}
         traffic_src = (f"no PMC profile of kernel build {ksha} with this launch layout for "
                        "this workload"
                        + (f"; refused profiles of other builds: {', '.join(stale[:3])}"
@@ -494,9 +517,15 @@ def main():
                                     "of added bytes chip-wide) plus the cold rows' plain stores "
                                     "(~6100 GB/s); peak = the update bytes over "
                                     "atomic/1300 + stored/6100",
-                "hbm_achieved_GBps": round(achieved, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
-                "hbm_frac": round(achieved / HBM_PEAK_GBPS, 4),
-                "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)",
+                # algorithmic bytes (every updated row read + written) against
+                # the HBM peak: a view, not measured HBM traffic
+                "alg_mem_achieved_GBps": round(achieved, 1), "hbm_peak_GBps": HBM_PEAK_GBPS,
+                "alg_mem_frac_of_hbm_peak": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic_unit": ("L2-to-fabric bytes per launch (Infinity Cache + HBM: PMC "
+                                 "TCC FETCH_SIZE x2 + WRITE_SIZE, which count the L2's "
+                                 "memory-side requests, Infinity-Cache hits included; "
+                                 "MI355X_MICROARCH.md 'HBM')"),
+                **counter_extras,
                 "traffic_source": traffic_src,
                 "kernel_src_sha16": ksha,
                 # waves that trained in the last timed launch (the stability
@@ -591,13 +620,20 @@ def main():
             "metric": METRIC, "value": round(value, 1), "unit": "pairs/s", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "scaling": a.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {
                 "workload": (f"{cfg_name}: synthetic Zipf({a.zipf:g}) gene pairs, V={V0}, "
                              f"{n_pairs} pairs, dim {D}, neg {K}, window 1, sample {a.sample:g}, "
-                             "1 epoch per step") if world == 1 else
-                            (f"C3: synthetic Zipf gene pairs, V={V0}, {n_pairs} pairs per GPU x "
-                             f"{world}, dim {D}, neg {K}, replica merge ({merge_rule}) every "
+                             "1 epoch per step") if world == 1 and a.scaling == "weak" else
+                            (f"C3 strong scaling: synthetic Zipf({a.zipf:g}) gene pairs, V={V0}, "
+                             f"{n_pairs * world} pairs in all, dim {D}, neg {K}, window 1, sample "
+                             f"{a.sample:g}, 1 epoch per step on one GPU") if world == 1 else
+                            ((f"C3 strong scaling: synthetic Zipf gene pairs, V={V0}, "
+                              f"{n_pairs * world} pairs in all = {n_pairs} per GPU x {world}"
+                              if a.scaling == "strong" else
+                              f"C3: synthetic Zipf gene pairs, V={V0}, {n_pairs} pairs per GPU x "
+                              f"{world}")
+                             + f", dim {D}, neg {K}, replica merge ({merge_rule}) every "
                              f"{avg_every} jobs: "
                              + (("libg2v g2v_average (RCCL over xGMI)" if a.backend == "nccl"
                                  else "libg2v RCCL merge path through G2V_RCCL_LIB (rehearsal, "
@@ -608,6 +644,7 @@ def main():
                                 if a.backend == "gloo" else
                                 "torch.distributed merge (libg2v communicator unavailable)")),
                 "vocab": V, "vocab_requested": V0, "zipf": a.zipf, "pairs_per_gpu": n_pairs,
+                **({"total_pairs": n_pairs * world} if a.scaling == "strong" else {}),
                 "dim": D, "negative": K, "sample": a.sample, "window": 1,
                 "parallelism": f"dp{world}" + (f" + {merge_backend} {merge_rule} merge"
                                                if world > 1 else "")},

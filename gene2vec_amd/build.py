@@ -84,10 +84,6 @@ def build(force: bool = False, verbose: bool = False, ablations: bool = False,
         out, objdir = ABLATIONS_LIB, os.path.join(HERE, "build", "ablations")
     else:
         out, objdir = LIB, os.path.join(HERE, "build")
-    if not force and not _stale(out):
-        return out
-    from concurrent.futures import ThreadPoolExecutor
-    os.makedirs(objdir, exist_ok=True)
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              # IEEE semantics: every fused multiply-add in the kernels is explicit
              "-ffp-contract=off", "-munsafe-fp-atomics", "-pthread",
@@ -95,6 +91,17 @@ def build(force: bool = False, verbose: bool = False, ablations: bool = False,
     if ablations:
         flags.append("-DG2V_ABLATIONS")
     flags += [f"-D{d}" for d in defines]
+    # the objects' compile flags are part of their key: a stamp in
+    # the object directory; another flag set rebuilds every object there
+    stamp = os.path.join(objdir, "flags.stamp")
+    key = " ".join(flags + ["|"] + list(SGNS_KERNEL_FLAGS) + list(kernel_flags))
+    old_key = open(stamp).read() if os.path.exists(stamp) else None
+    if old_key is not None and old_key != key:
+        force = True
+    if not force and not _stale(out):
+        return out
+    from concurrent.futures import ThreadPoolExecutor
+    os.makedirs(objdir, exist_ok=True)
     objs = [os.path.join(objdir, u[2]) for u in UNITS]
 
     def compile_one(i):
@@ -117,6 +124,8 @@ def build(force: bool = False, verbose: bool = False, ablations: bool = False,
         for err in ex.map(compile_one, range(len(UNITS))):
             if err and verbose:
                 print(err, file=sys.stderr)
+    with open(stamp, "w") as f:
+        f.write(key)
     tmp = out + ".tmp"
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-pthread", *objs, "-o", tmp]
     if verbose:

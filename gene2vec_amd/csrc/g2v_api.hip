@@ -151,9 +151,11 @@ struct g2v_ctx {
   int64_t stripe2_cap = 0;
   int atomic_overlap = 1;
   int tail_store = -1;  // G2V_OPT_TAIL_STORE: -1 auto (collision budget), 0 off, n rows >= n
-  // per row (index order) from set_vocab: u(r) = K p_neg(r) + p_tok(r) (syn1neg
-  // updates per example) and p_tok(r) (syn0), the tail stores' collision budget
-  std::vector<double> u_row, ptok_row;
+  // per row (index order) from set_vocab: the suffix max over rows >= r of
+  // u(r') = K p_neg(r') + p_tok(r') (syn1neg updates per example), the tail
+  // stores' collision budget; non-increasing whatever the count order or
+  // ns_exponent, so the auto boundary is a partition point
+  std::vector<double> u_row;
   int sample_overlap = 1;  // measured +1.2 % at C2
   int64_t merge_every = 0;  // G2V_OPT_MERGE_EVERY_JOBS: replica merges inside g2v_train
   int64_t debug_fail_merge = 0;  // G2V_OPT_DEBUG_FAIL_MERGE: fault injection
@@ -757,12 +759,12 @@ int g2v_set_option(g2v_ctx* c, int key, int64_t value) {
       c->sgns_grid = value > 0 ? (int)value : default_grid(c->cus, c->K, c->nv, c->u_max);
       return G2V_OK;
     case G2V_OPT_MERGE_BETA_MILLI:
-      REQUIRE(value >= 0 && value <= 1000, G2V_EINVAL, "merge beta (x1000) out of [0, 1000]");
+      REQUIRE(value >= 0 && value <= 4000, G2V_EINVAL, "merge beta (x1000) out of [0, 4000]");
       c->merge_beta = (float)value / 1000.0f;
       return G2V_OK;
     case G2V_OPT_MERGE_GAMMA_MILLI:
-      REQUIRE(value >= 1000 && value <= 16000, G2V_EINVAL,
-              "merge gamma (x1000) out of [1000, 16000]");
+      REQUIRE(value >= 250 && value <= 16000, G2V_EINVAL,
+              "merge gamma (x1000) out of [250, 16000]");
       c->merge_gamma = (float)value / 1000.0f;
       return G2V_OK;
     case G2V_OPT_RETIRED_19:
@@ -851,10 +853,10 @@ int g2v_set_vocab(g2v_ctx* c, const int64_t* counts, double sample, double ns_ex
     c->u_max = um;
     c->p_tok_max = pm;
     c->u_row.resize((size_t)c->V);
-    c->ptok_row.resize((size_t)c->V);
-    for (int32_t i = 0; i < c->V; ++i) {
-      c->u_row[i] = c->K * pn[i] / zn + pt[i] / zt;
-      c->ptok_row[i] = pt[i] / zt;
+    double suffix = 0.0;
+    for (int32_t i = c->V - 1; i >= 0; --i) {
+      suffix = std::max(suffix, c->K * pn[i] / zn + pt[i] / zt);
+      c->u_row[i] = suffix;
     }
     if (!c->grid_user) c->sgns_grid = default_grid(c->cus, c->K, c->nv, um);
   }
@@ -1195,7 +1197,7 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
                                         (int64_t)s.stripe_rows + max_rows2);
   const bool tier2 = striped &&
                      (c->debug_write == 0 || c->debug_write == 6 || c->debug_write == 8 ||
-                      c->debug_write == 9) &&
+                      c->debug_write == 9 || c->debug_write == 10) &&
                      r2 > s.stripe_rows;
   s.stripe2_rows = tier2 ? r2 : s.stripe_rows;
   s.stripe2_copies = tier2 ? c->stripe2_copies : 1;
@@ -1215,8 +1217,9 @@ static int run_sgns(g2v_ctx* c, const int64_t* n_examples_dev, int mode, bool ti
     if (c->tail_store < 0 && c->active_waves < kSgnsThreads / 64) {
       t0 = t1 = c->V;  // auto is off in the one-wave parity mode (G2V_OPT_ACTIVE_WAVES)
     } else if (c->tail_store < 0) {
-      // auto: the collision budget over the waves this launch may run
-      // (u(r), p_tok(r) are non-increasing in r: counts are sorted)
+      // auto: the collision budget over the waves this launch may run; the
+      // first row from which every later row is under it (u_row is a suffix
+      // max: a negative ns_exponent or unsorted counts put hot rows late)
       const double waves = (double)launch_grid(c) * c->active_waves;
       auto first_under = [&](const std::vector<double>& rate) {
         return (int)(std::partition_point(rate.begin(), rate.end(),

@@ -106,6 +106,23 @@ def kept_token_share(counts, sample):
     return kept / kept.sum()
 
 
+TAIL_COLLISION = 0.15  # kTailCollision in g2v_api.hip
+
+
+def tail_store_row(counts, sample, negative, waves, ns_exponent=0.75):
+    """first syn1neg row the auto cold-row stores (G2V_OPT_TAIL_STORE -1,
+    DESIGN.md 5e) write with plain stores: the first row r from which every
+    row r' >= r has waves x u(r') <= TAIL_COLLISION, u = K p_neg + p_tok (a
+    suffix max, so a negative ns_exponent or unsorted counts, which put hot
+    rows late, store nothing after them); len(counts) = none"""
+    v = np.asarray(counts, dtype=np.float64)
+    pn = v ** ns_exponent
+    u = negative * pn / pn.sum() + kept_token_share(v, sample)
+    suffix = np.maximum.accumulate(u[::-1])[::-1]
+    over = np.nonzero(waves * suffix > TAIL_COLLISION)[0]
+    return int(over[-1]) + 1 if len(over) else 0
+
+
 def count_ids(ids, V):
     ids = np.ascontiguousarray(ids, dtype=np.int32)
     counts = np.zeros(V, dtype=np.int64)

@@ -172,15 +172,18 @@ int g2v_set_stream(g2v_ctx *ctx, void *hip_stream);
  *                         the touch and align rules: new = old + sum_r d_r /
  *                         max(1, a^beta / gamma), a = the rule's count
  *                         (beta = gamma = 1: a itself; gamma > 1 scales the
- *                         step up, bounded by the sum); used by g2v_average,
+ *                         step up, bounded by the sum; beta > 1 or gamma < 1
+ *                         damps it; beta in [0, 4], gamma in [0.25, 16]);
+ *                         used by g2v_average,
  *                         the in-call merges and g2v_average_local (the first
  *                         context's) [1000, 1000]
  *   G2V_OPT_ACTIVE_WAVES  Hogwild kernel: waves per workgroup that train, 1..4;
  *                         with G2V_OPT_GRID 1 and 1 wave the production kernel
  *                         runs its chunks in record order, a deterministic
  *                         update order (parity checks) [4]
- *   G2V_OPT_TAIL_STORE    Hogwild kernel, vector_size <= 256 and negative <= 7
- *                         (DESIGN.md 5e): cold rows (never a striped row;
+ *   G2V_OPT_TAIL_STORE    Hogwild kernel, vector_size <= 512, any negative
+ *                         count, at most 8 stored syn1neg rows per example (the
+ *                         rest use atomics): cold rows (never a striped row;
  *                         syn1neg rows only in an example without a repeated
  *                         target) take plain write-through stores of their
  *                         new value instead of float atomics of the delta --

@@ -1,4 +1,4 @@
-"""Per-example HBM traffic of k_sgns_atomic from the PMC passes of
+"""Per-example L2-to-fabric traffic (Infinity Cache + HBM) of k_sgns_atomic from the PMC passes of
 scripts/profile_round.sh (rocprofv3 --pmc CSVs + the bench JSON of the same
 10 M-pair run).  FETCH_SIZE is doubled (gfx950 reports half the bytes of 16-B
 per-lane reads, MI355X_MICROARCH.md 'HBM'); WRITE_SIZE is exact for float
@@ -36,7 +36,7 @@ def bench_line(log):
 
 def main(out):
     c = {}
-    for i in range(1, 7):
+    for i in range(1, 10):
         if os.path.isdir(os.path.join(out, f"p{i}")):
             c.update(counters(os.path.join(out, f"p{i}")))
     b = bench_line(os.path.join(out, "p1.log"))
@@ -61,9 +61,13 @@ def main(out):
                   "WRITE_SIZE as is (KB units); summed over the SGNS launches / examples",
         "fetch_bytes_per_example": fetch, "write_bytes_per_example": write,
         "atomic_requests_per_example": c.get("TCC_EA0_ATOMIC_sum", 0.0) / ex,
-        "l2_hit_rate_incl_atomic_misses": hit / (hit + miss) if hit + miss else None,
+        # TCC_HIT / (TCC_HIT + TCC_MISS); the memory-side float atomics count as misses
+        "l2_hit_rate": hit / (hit + miss) if hit + miss else None,
         "examples_per_launch": ex / launches,
-        "hbm_bytes_per_launch": (fetch + write) * ex / launches,
+        # FETCH_SIZE / WRITE_SIZE count the L2's memory-side (fabric) requests:
+        # Infinity-Cache (MALL) hits are included, so this is not HBM traffic
+        # (MI355X_MICROARCH.md 'HBM'); no gfx950 counter splits MALL from HBM
+        "l2_fabric_bytes_per_launch": (fetch + write) * ex / launches,
         "algorithmic_bytes_per_example": bpe,
         "traffic_over_algorithmic": (fetch + write) / bpe,
     }
@@ -73,6 +77,24 @@ def main(out):
         res["ea_rdreq_to_mc_share"] = c["TCC_EA0_RDREQ_DRAM_sum"] / c["TCC_EA0_RDREQ_sum"]
     if "TCC_EA0_WRREQ_ATOMIC_DRAM_sum" in c and c.get("TCC_EA0_ATOMIC_sum"):
         res["ea_atomic_to_mc_share"] = c["TCC_EA0_WRREQ_ATOMIC_DRAM_sum"] / c["TCC_EA0_ATOMIC_sum"]
+    # VALU busy (the gfx94x VALUBusy formula, rocprofv3 has no gfx950 derived
+    # set): SQ_ACTIVE_INST_VALU x 4 / SIMDs / kernel cycles, the kernel's
+    # cycles = GRBM_GUI_ACTIVE / 8 (summed over the 8 XCDs, MI355X_MICROARCH.md
+    # 'DVFS give-back'); and the issue view, VALU wave-instructions x 4
+    # cycles (a wave64 op on a 16-lane SIMD) per SIMD-cycle
+    simds = 256 * 4
+    if c.get("GRBM_GUI_ACTIVE"):
+        cyc = c["GRBM_GUI_ACTIVE"] / 8.0
+        res["kernel_cycles_per_launch"] = cyc / launches
+        res["kernel_clock_GHz_per_launch_ms"] = None
+        if "SQ_ACTIVE_INST_VALU" in c:
+            res["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4.0 / simds / cyc
+        if "SQ_INSTS_VALU" in c:
+            res["valu_insts_per_cycle_per_simd"] = c["SQ_INSTS_VALU"] / simds / cyc
+            res["valu_issue_busy"] = 4.0 * c["SQ_INSTS_VALU"] / simds / cyc
+        if "SQ_BUSY_CYCLES" in c:
+            res["sq_busy_share"] = c["SQ_BUSY_CYCLES"] / c["GRBM_GUI_ACTIVE"]
+        res.pop("kernel_clock_GHz_per_launch_ms")
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
               "SQ_INSTS_LDS"):
         if k in c:  # wave-instructions per directed example

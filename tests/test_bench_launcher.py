@@ -49,3 +49,27 @@ def test_gpus_one_stays_one_process():
     out = json.loads(r.stdout.strip())
     assert out["n_gpus"] == 1 and out["rank_sum"] == 1
     assert "torch.distributed.run" not in r.stderr
+
+
+def test_strong_scaling_splits_the_total():
+    """--scaling strong (verdict r5 item 4): each of N ranks trains
+    --total-pairs / N (1 B / N by default); weak keeps 125 M per rank"""
+    for argv, n, per in ((["--gpus", "4", "--scaling", "strong"], 4, 250_000_000),
+                         (["--gpus", "2", "--scaling", "strong", "--total-pairs", "1000"], 2, 500),
+                         (["--gpus", "1", "--scaling", "strong"], 1, 1_000_000_000),
+                         (["--gpus", "2"], 2, 125_000_000),
+                         (["--gpus", "1"], 1, 100_000_000)):
+        r = subprocess.run([sys.executable, "bench.py", *argv, "--launch-probe"], cwd=ROOT,
+                           env=_env(), capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-3000:]
+        out = json.loads(r.stdout.strip())
+        assert out["n_gpus"] == n and out["rank_sum"] == out["ranks_expected_sum"]
+        assert out["pairs_per_rank"] == per, (argv, out)
+        assert out["scaling"] == ("strong" if "strong" in argv else "weak")
+
+
+def test_strong_scaling_refuses_pairs():
+    r = subprocess.run([sys.executable, "bench.py", "--scaling", "strong", "--pairs", "10",
+                        "--launch-probe"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and "--total-pairs" in r.stderr

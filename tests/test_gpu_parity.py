@@ -450,6 +450,43 @@ def test_train_hogwild_full_vocab_tracks_oracle():
     assert st["tail_row_syn0"] == -1, st
 
 
+@pytest.mark.parametrize("case", ["sorted", "ns_negative", "reversed"])
+def test_auto_tail_rows_follow_suffix_max(case):
+    """the auto cold-row boundary (G2V_OPT_TAIL_STORE -1) is the
+    first row from which every later row is under the collision budget --
+    with a negative ns_exponent or unsorted counts the hot rows sit late and
+    no row before them may take plain stores (engine.tail_store_row restates
+    the rule on the host)"""
+    D, K, sample = 200, 5, 1e-3
+    tok, counts, syn0 = _zipf_setup(400_000, 24447, D, K, sample)
+    V = len(counts)
+    ns = -0.75 if case == "ns_negative" else 0.75
+    if case == "reversed":
+        tok = (V - 1 - tok).astype(np.int32)
+        counts = counts[::-1].copy()
+        syn0 = syn0[::-1].copy()
+    n = len(tok) // 2
+    js = E.plan_jobs(n_sent=n, sent_len=2)
+    eng = E.SGNSEngine(V, D, K)
+    eng.set_vocab(counts, sample, ns_exponent=ns)
+    eng.set_weights(syn0, np.zeros((V, D), np.float32))
+    eng.set_corpus(tok, sent_len=2)
+    eng.train(js, E.job_alphas(js, n), E.job_seeds(np.random.RandomState(1), len(js) - 1),
+              N.MODE_HOGWILD)
+    st = eng.read_stats()
+    t = E.tail_store_row(counts, sample, K, st["sgns_grid"] * 4, ns_exponent=ns)
+    got = st["tail_row_syn1neg"]
+    if case == "sorted":
+        assert 0 < got < V
+    if t >= V:
+        assert got == -1, (st, t)
+    else:
+        assert abs(got - max(t, st["stripe2_rows"])) <= 1, (st, t)
+    assert st["tail_row_syn0"] == -1
+    g0, g1 = eng.get_weights()
+    assert np.isfinite(g0).all() and np.isfinite(g1).all()
+
+
 def test_striping_keeps_values_exact():
     """hot-row striping only changes where atomics land: with disjoint rows,
     striped == unstriped == sequential"""

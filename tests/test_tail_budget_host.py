@@ -41,3 +41,27 @@ def test_collision_budget_rows_at_c2():
     assert 1.4 < stored < 1.6
     # the budget is monotone: u(r) is non-increasing over the sorted counts
     assert np.all(np.diff(u) <= 1e-15)
+
+
+def test_tail_row_is_a_suffix_max_boundary():
+    """the auto boundary must hold for u(r) that is not
+    non-increasing -- a negative ns_exponent (rare genes drawn most as
+    negatives) or unsorted counts put hot rows late, and no row before the
+    last hot one may take plain stores"""
+    c = _zipf_counts(24447, 200_000_000)
+    t_sorted = E.tail_store_row(c, 1e-3, 5, 1024)
+    assert 7000 < t_sorted < 8500
+    # reversed counts: the hottest row is last, so nothing is stored
+    assert E.tail_store_row(c[::-1].copy(), 1e-3, 5, 1024) == len(c)
+    # negative exponent: the rarest rows carry the most negatives
+    t_neg = E.tail_store_row(c, 1e-3, 5, 1024, ns_exponent=-0.75)
+    pn = c.astype(np.float64) ** -0.75
+    u = 5 * pn / pn.sum() + E.kept_token_share(c, 1e-3)
+    assert np.all(1024 * u[t_neg:] <= 0.15)
+    assert t_neg == len(c) or 1024 * u[t_neg - 1:].max() > 0.15
+    # one hot row planted in the cold tail moves the boundary past it
+    c2 = c.copy()
+    c2[20000] = c2[0]
+    assert E.tail_store_row(c2, 1e-3, 5, 1024) == 20001
+    # a small vocabulary stores nothing at this budget
+    assert E.tail_store_row(_zipf_counts(3000, 2_000_000), 1e-3, 5, 1024) == 3000
