@@ -179,7 +179,10 @@ def ggipnn_auc(s0, index2word, pos_genes, seeds, device="cuda"):
                 if w in pos_genes:
                     f.write(w + "\t" + "".join(v + " " for v in s0[i].astype(np.float32)
                                                .astype(str)) + "\n")
-        return [G.train_and_auc(txt, DATA, seed=s, device=device) for s in seeds]
+        # the reference's classifier takes dim 200 (src/GGIPNN.py); other
+        # dims (C4: 512) size its embedding layer to the vectors
+        return [G.train_and_auc(txt, DATA, seed=s, device=device, embedding_size=s0.shape[1])
+                for s in seeds]
     finally:
         shutil.rmtree(out, ignore_errors=True)
 
