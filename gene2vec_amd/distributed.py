@@ -348,7 +348,7 @@ MERGE_RULES = {"touch": 0, "mean": 1, "align": 2}  # == G2V_MERGE_TOUCH / _MEAN 
 # every one of these arms.
 DP_TOUCH_MIN_PAIRS = 80_000_000
 DP_TOUCH_FIXED_PAIRS = 125_000_000
-DP_MIN_PAIRS = 80_000_000  # the CLI's --dp-min-pairs-per-rank default
+DP_MIN_PAIRS = 80_000_000  # smallest shard of every default window (DP_DEFAULT_WINDOWS)
 DP_MERGES_PER_EPOCH = 7
 DP_ALIGN_MERGES_PER_EPOCH = DP_MERGES_PER_EPOCH  # (round-3 name)
 DP_TOUCH_EVERY_JOBS = 3584
@@ -360,6 +360,45 @@ DP_TOUCH_EVERY_JOBS = 3584
 # held-out and GGIPNN AUC within 0.4 % everywhere.  So up to this many ranks
 # the plan merges once per epoch (the epoch call's last window).
 DP_EPOCH_MERGE_MAX_WORLD = 4
+
+# Where the CLI shards by DEFAULT (round 6, verdict r5 item 1):
+# the world sizes and pairs-per-rank windows where the plan above was measured
+# within 1 % of one model on the target function on BOTH corpora (A: Zipf 1.0,
+# 1,000 modules; B: Zipf 1.2, 600 modules), held-in / held-out / AUC within
+# 0.7 % there too:
+#   3 ranks: 80 M +0.48 / +0.40 %, 100 M +0.54 / +0.92 %
+#   4 ranks: 80 M -0.36 / -0.63 %, 100 M +0.07 / +0.32..+0.43 %; 125 M reads
+#            +0.33 / +1.30 % (B out), so the window stops at 100 M
+#   8 ranks: 80 M -0.97 % (A), 125 M +0.70 % / -0.71..-1.02 % (B, four runs,
+#            mean -0.88 %): from 80 M up
+# and nowhere else: at 2 ranks the merged model leads one model on B by
+# +1.1..+2.6 % (80 M, 125 M) with every rule and cadence of round 5; a damped
+# divisor k^1.5 brings 2 x 80 M in (+0.80 / -0.84 %) but leaves 2 x 125 M B at
+# +1.16 % and beta 2 overshoots to -1.7..-4.3 %, so no one rule holds both
+# shard sizes; at 6 ranks the 8-rank plan reads +1.91 % (A, 125 M) and
+# -1.66 % (B, 80 M); 5 and 7 ranks are unmeasured.  Outside these windows
+# every rank trains the whole corpus unless the user sets
+# --dp-min-pairs-per-rank (then: shard from that many pairs per rank, any
+# world, with the plan above).
+DP_DEFAULT_WINDOWS = {3: (80_000_000, 100_000_000), 4: (80_000_000, 100_000_000),
+                      8: (80_000_000, None)}
+
+
+def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):
+    """True when the CLI shards `n_pairs` over `world` ranks: inside the
+    measured window of DP_DEFAULT_WINDOWS for that world by default; with an
+    explicit min_pairs_per_rank (--dp-min-pairs-per-rank), from that many pairs
+    per rank at any world size"""
+    if world <= 1:
+        return False
+    per = n_pairs / world
+    if min_pairs_per_rank is not None:
+        return per >= min_pairs_per_rank
+    win = DP_DEFAULT_WINDOWS.get(world)
+    if win is None:
+        return False
+    lo, hi = win
+    return per >= lo and (hi is None or per <= hi)
 
 
 def dp_merge_plan(pairs_per_rank, merge_every_jobs=None, rule="auto", jobs_per_rank=None,

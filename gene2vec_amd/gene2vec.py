@@ -253,13 +253,15 @@ def main(argv=None):
                         help="data-parallel merge: libg2v over RCCL (nccl) or over the host "
                              "collective (gloo) = auto; torch = torch-owned tables merged by "
                              "torch.distributed")
-    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=80_000_000,
-                        help="under torchrun, shard the pairs only when every rank gets at least "
-                             "this many; a smaller corpus trains whole on every rank (no merges, "
-                             "rank 0 writes).  80 M is the smallest shard where a measured merge "
-                             "rule holds the target function within 1 %% of one model (DESIGN.md "
-                             "7b); 50 M .. 80 M (align rule, up to +2 %% there) and anything "
-                             "below (-2.6 %% at best) are explicit opt-ins")
+    parser.add_argument("--dp-min-pairs-per-rank", type=int, default=None,
+                        help="under torchrun, shard the pairs when every rank gets at least "
+                             "this many (any world size); a smaller corpus trains whole on every "
+                             "rank (no merges, rank 0 writes).  Default: shard only where the "
+                             "merge plan was measured within 1 %% of one model on the target "
+                             "function on both test corpora (DESIGN.md 7a): 3 or 4 ranks with "
+                             "80-100 M pairs per rank, 8 ranks from 80 M; never at 2 ranks "
+                             "(+1.1..+2.6 %% there) nor at 5-7 (6 ranks: up to +1.9 %%).  Setting "
+                             "it is an opt-in to those gaps")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "
@@ -336,10 +338,16 @@ def main(argv=None):
             pipe = ingest.ShufflePipeline(corpus.n_sent, rng, max(1, args.iters))
     # data parallelism only for corpora big enough that merged replicas match
     # one model; below, every rank trains the whole corpus
-    shard = world > 1 and n_pairs >= world * args.dp_min_pairs_per_rank
+    from . import distributed as Dd
+    shard = Dd.dp_default_shard(n_pairs, world, args.dp_min_pairs_per_rank)
     if world > 1 and not shard:
-        print(f"{n_pairs} pairs < {world} ranks x {args.dp_min_pairs_per_rank}: every rank "
-              "trains the whole corpus (no sharding, no merges); rank 0 writes the outputs")
+        why = (f"< {world} ranks x {args.dp_min_pairs_per_rank}"
+               if args.dp_min_pairs_per_rank is not None else
+               f"over {world} ranks is outside the measured data-parallel windows "
+               f"{ {w: Dd.DP_DEFAULT_WINDOWS[w] for w in sorted(Dd.DP_DEFAULT_WINDOWS)} } "
+               "(pairs per rank; DESIGN.md 7a)")
+        print(f"{n_pairs} pairs {why}: every rank trains the whole corpus (no sharding, no "
+              "merges); rank 0 writes the outputs")
     drank, dworld = (rank, world) if shard else (0, 1)
     dorder = None
     perm_seed = None

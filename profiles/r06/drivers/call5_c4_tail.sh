@@ -23,3 +23,11 @@ for T in -1 30000 45000 0; do
     || { echo "bench $T failed"; tail -5 gpurun_out/r06_c4_bench_tail$T.err; exit 1; }
   python3 -c "import json;d=json.load(open('gpurun_out/r06_c4_bench_tail$T.json'));r=d['roofline'];print('tail $T',d['value'],r['avg_launch_ms'],r['stored_rows_per_example'],r['tail_row_syn1neg'])"
 done
+# 8 ranks x 80 M pairs on corpus B (the 8-rank window's low end; corpus A was measured in round 4)
+timeout -k 10 500 python -u scripts/replica_quality.py --replicas 8 --pairs-per-replica 80000000 \
+  --iters 10 --ggipnn-repeat 3 --modules 600 --p-module 0.3 --zipf 1.2 --merge-every 2286 \
+  --replica-seeds 1 --single-seeds 1 --auc-seeds 0 --rules touch --out gpurun_out/rq_r06_s80_n8_B \
+  > gpurun_out/r06_rq_s80_n8_B.log 2>&1 || { echo "study 8x80M B failed"; tail -20 gpurun_out/r06_rq_s80_n8_B.log; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/rq_r06_s80_n8_B/replica_quality.json'))
+for t, r in d['runs'].items(): print('8x80M B', t, {k: r[k] for k in r if k.endswith('gap')})"

@@ -20,10 +20,11 @@ def _parsed(argv):
 
 def test_cli_defaults_match_the_c3_gate():
     """tests/test_gpu_c3_quality.py runs the CLI's defaults: a merge every 3,584
-    jobs from 125 M pairs per rank and sharding from 50 M; the reference's own settings
+    jobs from 125 M pairs per rank, sharding only in the measured windows
+    (distributed.DP_DEFAULT_WINDOWS); the reference's own settings
     (src/gene2vec.py:57-63) stay the CLI's"""
     a = _parsed(["d", "o", "txt"])
-    assert a["merge_every_jobs"] is None and a["dp_min_pairs_per_rank"] == 80_000_000
+    assert a["merge_every_jobs"] is None and a["dp_min_pairs_per_rank"] is None
     assert a["merge_rule"] == "auto"
     assert (a["dim"], a["negative"], a["window"], a["sample"], a["iters"], a["workers"]) == \
         (200, 5, 1, 1e-3, 10, 32)
@@ -73,3 +74,33 @@ def test_dp_merge_plan_by_world_size():
     assert Dd.dp_merge_plan(125_000_000, world=5) == ("touch", 3584)
     assert Dd.dp_merge_plan(125_000_000, world=8) == ("touch", 3584)
     assert Dd.dp_merge_plan(125_000_000, jobs_per_rank=25_088, world=4) == ("touch", 25_088)
+
+
+def test_default_shard_windows():
+    """verdict r5 item 1: the CLI shards by default only at the world sizes and
+    pairs per rank where the merge plan was measured within 1 % of one model
+    on both test corpora; --dp-min-pairs-per-rank opts in"""
+    from gene2vec_amd import distributed as Dd
+    M = 1_000_000
+    # 2 ranks: never by default (the merged model leads by 1.1-2.6 % on corpus B)
+    for per in (50 * M, 80 * M, 125 * M, 500 * M):
+        assert not Dd.dp_default_shard(2 * per, 2)
+    # 3 and 4 ranks: 80-100 M pairs per rank
+    for w in (3, 4):
+        assert not Dd.dp_default_shard(w * 79 * M, w)
+        assert Dd.dp_default_shard(w * 80 * M, w) and Dd.dp_default_shard(w * 100 * M, w)
+        assert not Dd.dp_default_shard(w * 101 * M, w) and not Dd.dp_default_shard(w * 125 * M, w)
+    # 5-7 ranks: never by default; 8 ranks from 80 M up
+    for w in (5, 6, 7):
+        assert not Dd.dp_default_shard(w * 125 * M, w)
+    assert not Dd.dp_default_shard(8 * 79 * M, 8)
+    assert Dd.dp_default_shard(8 * 80 * M, 8) and Dd.dp_default_shard(8 * 1000 * M, 8)
+    assert not Dd.dp_default_shard(10 ** 9, 1) and not Dd.dp_default_shard(16 * 125 * M, 16)
+    # the explicit threshold: any world size from that many pairs per rank
+    assert Dd.dp_default_shard(2 * 125 * M, 2, 50 * M)
+    assert Dd.dp_default_shard(6 * 10, 6, 0)
+    assert not Dd.dp_default_shard(2 * 40 * M, 2, 50 * M)
+    # the plans the windows were measured with
+    assert Dd.dp_merge_plan(100 * M, world=4) == ("touch", 20000)
+    assert Dd.dp_merge_plan(80 * M, world=3) == ("touch", 16000)
+    assert Dd.dp_merge_plan(125 * M, world=8) == ("touch", 3584)
