@@ -5,12 +5,12 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -v --timeout 600 --timeout-method thread \
+  tests/test_gpu_c3_quality.py -k small_world > gpurun_out/r06_c3_window_tests.log 2>&1 \
+  || { echo "window gates failed"; tail -30 gpurun_out/r06_c3_window_tests.log; exit 1; }
+grep -E "PASS|FAIL|replicas x|passed|failed" gpurun_out/r06_c3_window_tests.log | tail -8
 bash scripts/profile_round.sh r06_c2 > gpurun_out/r06_prof_c2.log 2>&1 || { echo "c2 profile failed"; tail -20 gpurun_out/r06_prof_c2.log; exit 1; }
 tail -3 gpurun_out/r06_prof_c2.log
-bash scripts/profile_round.sh r06_c4 --vocab 60000 --dim 512 --negative 15 > gpurun_out/r06_prof_c4.log 2>&1 || { echo "c4 profile failed"; tail -20 gpurun_out/r06_prof_c4.log; exit 1; }
-tail -3 gpurun_out/r06_prof_c4.log
-bash scripts/profile_round.sh r06_s0 --sample 0 > gpurun_out/r06_prof_s0.log 2>&1 || { echo "s0 profile failed"; tail -20 gpurun_out/r06_prof_s0.log; exit 1; }
-tail -3 gpurun_out/r06_prof_s0.log
 timeout -k 10 300 python -u scripts/lost_updates.py --tails auto --out gpurun_out/r06_lost_auto.json \
   > gpurun_out/r06_lost.log 2>&1 || { echo "lost-update probe failed"; tail -20 gpurun_out/r06_lost.log; exit 1; }
 tail -5 gpurun_out/r06_lost.log
