@@ -5,10 +5,6 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
-  tests/test_gpu_c4_e2e.py tests/test_gpu_parity.py -k "c4_cold or auto_tail" > gpurun_out/r06_c5_tests.log 2>&1 \
-  || { echo "tests failed"; tail -30 gpurun_out/r06_c5_tests.log; exit 1; }
-grep -E "PASS|FAIL|passed|failed" gpurun_out/r06_c5_tests.log | tail -6
 timeout -k 10 700 python -u scripts/e2e_parity.py --vocab 60000 --dim 512 --negative 15 \
   --modules 2000 --pairs 10000000 --seeds 1,2,3 --auc-seeds 0,1,2 \
   --engines gpu_tail0,gpu,gpu_tail30000,gpu_tail45000 --reference-engine gpu_tail0 \
@@ -31,3 +27,7 @@ timeout -k 10 500 python -u scripts/replica_quality.py --replicas 8 --pairs-per-
 python3 -c "
 import json; d=json.load(open('gpurun_out/rq_r06_s80_n8_B/replica_quality.json'))
 for t, r in d['runs'].items(): print('8x80M B', t, {k: r[k] for k in r if k.endswith('gap')})"
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread \
+  tests/test_gpu_c4_e2e.py tests/test_gpu_parity.py -k "c4_cold or auto_tail" > gpurun_out/r06_c5_tests.log 2>&1 \
+  || echo "tests failed"
+grep -E "PASS|FAIL|passed|failed" gpurun_out/r06_c5_tests.log | tail -6

@@ -9,8 +9,10 @@ permutation of the pairs and the alpha sawtooth restarting every train()
 call) on a planted-module corpus of that shape, once with the default stores
 and once with every row atomic (G2V_OPT_TAIL_STORE 0), and requires the
 manuscript target function (src/evaluation_target_function.py:16-60, the
-modules as pathways) within 1 % and the held-in SGNS objective within 0.5 %
-(the bars of tests/test_gpu_e2e_parity.py).
+modules as pathways) and the held-in SGNS objective within north_star's 1 %
+(measured: -0.66 % and +0.38 %, a systematic shift beyond the seeds' own
+spread of 0.02 % / 0.35 %; storing fewer rows shrinks it, at a cost in
+throughput: DESIGN.md 5e).
 The full-size comparison against the C restatement's 16-thread Hogwild is
 scripts/e2e_parity.py (profiles/r06/e2e_c4/).
 """
@@ -101,11 +103,12 @@ def test_c4_cold_row_stores_keep_target_function(corpus):
             assert st["tail_row_syn0"] == -1
             assert np.isfinite(s0).all() and np.isfinite(s1).all()
             tg.append(RQ.target_of(s0, index2word, vc, gmt, D)["ratio"])
-            hi.append(RQ.heldin(s0, s1, tok0, vc, K, n=20000))
+            hi.append(RQ.heldin(s0, s1, tok0, vc, K))
         res[arm] = (float(np.mean(tg)), float(np.mean(hi)))
     (t_s, h_s), (t_a, h_a) = res["stores"], res["atomic"]
     assert t_a > 2.0, res  # the modules are learned (measured 2.43)
-    # measured at this corpus: target -0.67 %, objective +0.39 % (stores vs
-    # atomics, two seeds each; the seeds' own spread 0.1 % / 0.5 %)
+    # measured at this corpus (three seeds each, profiles/r06/e2e_c4_tail/):
+    # stores vs atomics target -0.66 %, objective +0.38 %; the seeds' own
+    # spread 0.02 % / 0.35 %; north_star's bar is 1 %
     assert abs(t_s - t_a) / t_a < 0.01, res
-    assert abs(h_s - h_a) / h_a < 0.005, res
+    assert abs(h_s - h_a) / h_a < 0.01, res
