@@ -369,8 +369,11 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 #   3 ranks: 80 M +0.48 / +0.40 %, 100 M +0.54 / +0.92 %
 #   4 ranks: 80 M -0.36 / -0.63 %, 100 M +0.07 / +0.32..+0.43 %; 125 M reads
 #            +0.33 / +1.30 % (B out), so the window stops at 100 M
-#   8 ranks: 80 M -0.97 % (A), 125 M +0.70 % / -0.71..-1.02 % (B, four runs,
-#            mean -0.88 %): from 80 M up
+#   8 ranks: 125 M +0.70 % / -0.71..-1.02 % (B, four runs, mean -0.88 %);
+#            80 M -0.97 / -4.49 %, 150 M +1.25 / +0.06 %, 250 M +2.27 / +1.87 %
+#            (7 merges per epoch; +4.15 / +3.31 % every 3,584 jobs): the
+#            window is 120-135 M, the C3 shard (1 B pairs over 8) inside it,
+#            its edges interpolated between 80, 125 and 150 M
 # and nowhere else: at 2 ranks the merged model leads one model on B by
 # +1.1..+2.6 % (80 M, 125 M) with every rule and cadence of round 5; a damped
 # divisor k^1.5 brings 2 x 80 M in (+0.80 / -0.84 %) but leaves 2 x 125 M B at
@@ -381,7 +384,7 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 # --dp-min-pairs-per-rank (then: shard from that many pairs per rank, any
 # world, with the plan above).
 DP_DEFAULT_WINDOWS = {3: (80_000_000, 100_000_000), 4: (80_000_000, 100_000_000),
-                      8: (80_000_000, None)}
+                      8: (120_000_000, 135_000_000)}
 
 
 def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):

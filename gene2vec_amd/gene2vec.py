@@ -259,9 +259,10 @@ def main(argv=None):
                              "rank (no merges, rank 0 writes).  Default: shard only where the "
                              "merge plan was measured within 1 %% of one model on the target "
                              "function on both test corpora (DESIGN.md 7a): 3 or 4 ranks with "
-                             "80-100 M pairs per rank, 8 ranks from 80 M; never at 2 ranks "
-                             "(+1.1..+2.6 %% there) nor at 5-7 (6 ranks: up to +1.9 %%).  Setting "
-                             "it is an opt-in to those gaps")
+                             "80-100 M pairs per rank, 8 ranks with 120-135 M (C3: 1 B pairs); "
+                             "never at 2 ranks (+1.1..+2.6 %% there) nor at 5-7 (6 ranks: up to "
+                             "+1.9 %%); 8 x 80 M reads -4.5 %%, 8 x 250 M +2.3 %%.  Setting it is "
+                             "an opt-in to those gaps")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "

@@ -90,11 +90,12 @@ def test_default_shard_windows():
         assert not Dd.dp_default_shard(w * 79 * M, w)
         assert Dd.dp_default_shard(w * 80 * M, w) and Dd.dp_default_shard(w * 100 * M, w)
         assert not Dd.dp_default_shard(w * 101 * M, w) and not Dd.dp_default_shard(w * 125 * M, w)
-    # 5-7 ranks: never by default; 8 ranks from 80 M up
+    # 5-7 ranks: never by default; 8 ranks around C3's 125 M per rank
     for w in (5, 6, 7):
         assert not Dd.dp_default_shard(w * 125 * M, w)
-    assert not Dd.dp_default_shard(8 * 79 * M, 8)
-    assert Dd.dp_default_shard(8 * 80 * M, 8) and Dd.dp_default_shard(8 * 1000 * M, 8)
+    assert Dd.dp_default_shard(10 ** 9, 8)  # C3: 1 B pairs over 8 GPUs
+    for per in (80, 100, 119, 136, 150, 250):
+        assert not Dd.dp_default_shard(8 * per * M, 8), per
     assert not Dd.dp_default_shard(10 ** 9, 1) and not Dd.dp_default_shard(16 * 125 * M, 16)
     # the explicit threshold: any world size from that many pairs per rank
     assert Dd.dp_default_shard(2 * 125 * M, 2, 50 * M)
