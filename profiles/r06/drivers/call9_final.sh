@@ -5,6 +5,10 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r06final
 mkdir -p $O
+# the counters this gfx950 exposes (looking for an Infinity-Cache / HBM split)
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+timeout -k 10 120 rocprofv3 -L > $O/counters_list.txt 2>&1 || echo "counter listing failed"
+grep -i -E "mall|dram|hbm|infinity|_ea0_|df_" $O/counters_list.txt | head -40
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 700 --timeout-method thread > $O/gpu_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/gpu_tests.log | tail -4
 [ $rc -eq 0 ] || exit 1

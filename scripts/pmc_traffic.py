@@ -86,15 +86,11 @@ def main(out):
     if c.get("GRBM_GUI_ACTIVE"):
         cyc = c["GRBM_GUI_ACTIVE"] / 8.0
         res["kernel_cycles_per_launch"] = cyc / launches
-        res["kernel_clock_GHz_per_launch_ms"] = None
         if "SQ_ACTIVE_INST_VALU" in c:
             res["valu_busy"] = c["SQ_ACTIVE_INST_VALU"] * 4.0 / simds / cyc
         if "SQ_INSTS_VALU" in c:
             res["valu_insts_per_cycle_per_simd"] = c["SQ_INSTS_VALU"] / simds / cyc
             res["valu_issue_busy"] = 4.0 * c["SQ_INSTS_VALU"] / simds / cyc
-        if "SQ_BUSY_CYCLES" in c:
-            res["sq_busy_share"] = c["SQ_BUSY_CYCLES"] / c["GRBM_GUI_ACTIVE"]
-        res.pop("kernel_clock_GHz_per_launch_ms")
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_VMEM_WR", "SQ_INSTS_VMEM_RD",
               "SQ_INSTS_LDS"):
         if k in c:  # wave-instructions per directed example
