@@ -369,11 +369,15 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 #   3 ranks: 80 M +0.48 / +0.40 %, 100 M +0.54 / +0.92 %
 #   4 ranks: 80 M -0.36 / -0.63 %, 100 M +0.07 / +0.32..+0.43 %; 125 M reads
 #            +0.33 / +1.30 % (B out), so the window stops at 100 M
-#   8 ranks: 125 M +0.70 % / -0.71..-1.02 % (B, four runs, mean -0.88 %);
-#            80 M -0.97 / -4.49 %, 150 M +1.25 / +0.06 %, 250 M +2.27 / +1.87 %
-#            (7 merges per epoch; +4.15 / +3.31 % every 3,584 jobs): the
-#            window is 120-135 M, the C3 shard (1 B pairs over 8) inside it,
-#            its edges interpolated between 80, 125 and 150 M
+#   8 ranks: the wide-shard plan below (touch, DP_WIDE_MERGE_PAIRS / shard
+#            merges per epoch): 150 M (5 per epoch) +0.44 / -0.58 %, 200 M (4)
+#            +0.85 / +0.55 %; 250 M (3) +0.90 / +0.69 % but B's held-in
+#            objective -1.56 % (the replicas fit their pairs better), so the
+#            window stops at 200 M.  Not C3's 125 M:
+#            there corpus B reads -1.12..-1.23 % on the round-6 kernel at
+#            every 3,584 or 3,328 jobs (A +0.70..+0.87 %), 120 M -0.81 %,
+#            135 M A +1.11 %; 80 M -0.97 / -4.49 %; at 7 merges per epoch
+#            150 M +1.25 / +0.06 %, 250 M +2.27 / +1.87 % (14: +4.15 / +3.31 %)
 # and nowhere else: at 2 ranks the merged model leads one model on B by
 # +1.1..+2.6 % (80 M, 125 M) with every rule and cadence of round 5; a damped
 # divisor k^1.5 brings 2 x 80 M in (+0.80 / -0.84 %) but leaves 2 x 125 M B at
@@ -384,7 +388,16 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 # --dp-min-pairs-per-rank (then: shard from that many pairs per rank, any
 # world, with the plan above).
 DP_DEFAULT_WINDOWS = {3: (80_000_000, 100_000_000), 4: (80_000_000, 100_000_000),
-                      8: (120_000_000, 135_000_000)}
+                      8: (150_000_000, 200_000_000)}
+
+# Wide shards beyond 4 ranks (round 6): at 8 ranks and 7 merges
+# per epoch the two corpora's target-function gaps grow with the shard but
+# draw together (A - B: 3.5 % at 80 M, 1.9 % at 125 M, 1.2 % at 150 M, 0.4 %
+# at 250 M) and fewer merges lower both, so from DP_WIDE_MIN_PAIRS pairs per
+# rank the plan merges round(DP_WIDE_MERGE_PAIRS / pairs per rank) times per
+# epoch (150 M: 5, 200 M: 4, 250 M: 3)
+DP_WIDE_MIN_PAIRS = 150_000_000
+DP_WIDE_MERGE_PAIRS = 750_000_000
 
 
 def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):
@@ -408,7 +421,9 @@ def dp_merge_plan(pairs_per_rank, merge_every_jobs=None, rule="auto", jobs_per_r
                   world=8):
     """(rule, merge_every_jobs) for a data-parallel run of `world` ranks.
     rule "auto": up to DP_EPOCH_MERGE_MAX_WORLD ranks, touch once per epoch;
-    beyond, touch every merge_every_jobs (default DP_TOUCH_EVERY_JOBS) from
+    beyond, from DP_WIDE_MIN_PAIRS pairs per rank touch at
+    round(DP_WIDE_MERGE_PAIRS / pairs per rank) merges per epoch, below that
+    touch every merge_every_jobs (default DP_TOUCH_EVERY_JOBS) from
     DP_TOUCH_FIXED_PAIRS pairs per rank, touch at DP_MERGES_PER_EPOCH merges
     per epoch (or merge_every_jobs, if more often) from DP_TOUCH_MIN_PAIRS, and
     align at DP_MERGES_PER_EPOCH merges per epoch below (jobs_per_rank: gensim
@@ -420,6 +435,9 @@ def dp_merge_plan(pairs_per_rank, merge_every_jobs=None, rule="auto", jobs_per_r
         return rule, int(merge_every_jobs or DP_TOUCH_EVERY_JOBS)
     if world <= DP_EPOCH_MERGE_MAX_WORLD:
         return "touch", int(merge_every_jobs or max(1, int(jobs_per_rank)))
+    if pairs_per_rank >= DP_WIDE_MIN_PAIRS and not merge_every_jobs:
+        merges = max(1, int(round(DP_WIDE_MERGE_PAIRS / float(pairs_per_rank))))
+        return "touch", max(1, -(-int(jobs_per_rank) // merges))
     every = int(merge_every_jobs or DP_TOUCH_EVERY_JOBS)
     if pairs_per_rank >= DP_TOUCH_FIXED_PAIRS:
         return "touch", every

@@ -238,14 +238,16 @@ def main(argv=None):
                              "is the same state: tables, vocabulary and RNG round-trip exactly)")
     parser.add_argument("--merge-every-jobs", type=int, default=None,
                         help="data-parallel replica merge cadence (gensim jobs per rank); "
-                             "default: the plan's -- once per epoch up to 4 ranks, every 3,584 "
-                             "jobs (7 merges per epoch at C3) beyond (DESIGN.md 7a)")
+                             "default: the plan's -- once per epoch up to 4 ranks; beyond, "
+                             "round(750 M / pairs per rank) merges per epoch from 150 M pairs per "
+                             "rank, every 3,584 jobs from 125 M (DESIGN.md 7a)")
     parser.add_argument("--merge-rule", choices=("auto", "touch", "align", "mean"),
                         default="auto",
                         help="data-parallel replica merge rule: auto = touch once per epoch "
-                             "up to 4 ranks; beyond, touch every --merge-every-jobs jobs from "
-                             "125 M pairs per rank, touch at 7 merges per epoch from 80 M, align "
-                             "at 7 merges per epoch below (only with a lowered "
+                             "up to 4 ranks; beyond, from 150 M pairs per rank touch at "
+                             "round(750 M / pairs per rank) merges per epoch, from 125 M every "
+                             "--merge-every-jobs jobs, from 80 M at 7 merges per epoch, align at 7 "
+                             "merges per epoch below (below 150 M only with "
                              "--dp-min-pairs-per-rank; DESIGN.md 7a/7b); an explicit rule uses "
                              "--merge-every-jobs (default 3,584)")
     parser.add_argument("--merge-transport", choices=("auto", "rccl", "host", "torch"),
@@ -259,10 +261,10 @@ def main(argv=None):
                              "rank (no merges, rank 0 writes).  Default: shard only where the "
                              "merge plan was measured within 1 %% of one model on the target "
                              "function on both test corpora (DESIGN.md 7a): 3 or 4 ranks with "
-                             "80-100 M pairs per rank, 8 ranks with 120-135 M (C3: 1 B pairs); "
-                             "never at 2 ranks (+1.1..+2.6 %% there) nor at 5-7 (6 ranks: up to "
-                             "+1.9 %%); 8 x 80 M reads -4.5 %%, 8 x 250 M +2.3 %%.  Setting it is "
-                             "an opt-in to those gaps")
+                             "80-100 M pairs per rank, 8 ranks with 150-200 M; never at 2 ranks "
+                             "(+1.1..+2.6 %% there) nor at 5-7 (6 ranks: up to +1.9 %%); C3's 8 x "
+                             "125 M reads -1.1..-1.2 %% on one corpus, 8 x 80 M -4.5 %%.  Setting "
+                             "it is an opt-in to those gaps")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "

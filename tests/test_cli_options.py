@@ -90,12 +90,15 @@ def test_default_shard_windows():
         assert not Dd.dp_default_shard(w * 79 * M, w)
         assert Dd.dp_default_shard(w * 80 * M, w) and Dd.dp_default_shard(w * 100 * M, w)
         assert not Dd.dp_default_shard(w * 101 * M, w) and not Dd.dp_default_shard(w * 125 * M, w)
-    # 5-7 ranks: never by default; 8 ranks around C3's 125 M per rank
+    # 5-7 ranks: never by default; 8 ranks with 150-200 M pairs per rank (not
+    # C3's 125 M, where corpus B reads -1.1..-1.2 %)
     for w in (5, 6, 7):
-        assert not Dd.dp_default_shard(w * 125 * M, w)
-    assert Dd.dp_default_shard(10 ** 9, 8)  # C3: 1 B pairs over 8 GPUs
-    for per in (80, 100, 119, 136, 150, 250):
+        assert not Dd.dp_default_shard(w * 200 * M, w)
+    assert not Dd.dp_default_shard(10 ** 9, 8)
+    for per in (80, 125, 149, 201, 250, 500):
         assert not Dd.dp_default_shard(8 * per * M, 8), per
+    for per in (150, 175, 200):
+        assert Dd.dp_default_shard(8 * per * M, 8), per
     assert not Dd.dp_default_shard(10 ** 9, 1) and not Dd.dp_default_shard(16 * 125 * M, 16)
     # the explicit threshold: any world size from that many pairs per rank
     assert Dd.dp_default_shard(2 * 125 * M, 2, 50 * M)
@@ -105,3 +108,8 @@ def test_default_shard_windows():
     assert Dd.dp_merge_plan(100 * M, world=4) == ("touch", 20000)
     assert Dd.dp_merge_plan(80 * M, world=3) == ("touch", 16000)
     assert Dd.dp_merge_plan(125 * M, world=8) == ("touch", 3584)
+    # wide shards: round(750 M / pairs per rank) merges per epoch
+    assert Dd.dp_merge_plan(150 * M, world=8) == ("touch", 6000)       # 5
+    assert Dd.dp_merge_plan(200 * M, world=8) == ("touch", 10000)      # 4
+    assert Dd.dp_merge_plan(250 * M, world=8) == ("touch", 16667)      # 3
+    assert Dd.dp_merge_plan(150 * M, 2048, world=8) == ("touch", 2048)  # explicit kept
