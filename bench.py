@@ -353,6 +353,9 @@ def main():
     step_seeds = [E.job_seeds(rs, n_jobs) for _ in range(a.warmup + a.steps)]
     merge_rule, avg_every = Dd.dp_merge_plan(n_pairs, a.avg_every_jobs or None, a.merge,
                                              jobs_per_rank=n_jobs, world=world)
+    merge_beta = Dd.dp_merge_beta(n_pairs, world, a.merge)
+    if merge_beta != 1.0:
+        eng.set_option(N.OPT_MERGE_BETA_MILLI, int(round(merge_beta * 1000)))
     if not use_dist:
         avg_every = n_jobs
     merge_backend = "torch"

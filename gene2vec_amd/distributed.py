@@ -378,16 +378,17 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 #            every 3,584 or 3,328 jobs (A +0.70..+0.87 %), 120 M -0.81 %,
 #            135 M A +1.11 %; 80 M -0.97 / -4.49 %; at 7 merges per epoch
 #            150 M +1.25 / +0.06 %, 250 M +2.27 / +1.87 % (14: +4.15 / +3.31 %)
-# and nowhere else: at 2 ranks the merged model leads one model on B by
-# +1.1..+2.6 % (80 M, 125 M) with every rule and cadence of round 5; a damped
-# divisor k^1.5 brings 2 x 80 M in (+0.80 / -0.84 %) but leaves 2 x 125 M B at
-# +1.16 % and beta 2 overshoots to -1.7..-4.3 %, so no one rule holds both
-# shard sizes; at 6 ranks the 8-rank plan reads +1.91 % (A, 125 M) and
+#   2 ranks: the touch divisor damped to k^beta, beta rising with the shard
+#            (DP_BETA_SCHEDULE below): 80-200 M within 0.9 % at every
+#            measured point (undamped the merged model leads one model on B
+#            by +1.1..+2.6 %, and no one beta holds 80 and 125 M)
+# and nowhere else: at 6 ranks the 8-rank plan reads +1.91 % (A, 125 M) and
 # -1.66 % (B, 80 M); 5 and 7 ranks are unmeasured.  Outside these windows
 # every rank trains the whole corpus unless the user sets
 # --dp-min-pairs-per-rank (then: shard from that many pairs per rank, any
 # world, with the plan above).
-DP_DEFAULT_WINDOWS = {3: (80_000_000, 100_000_000), 4: (80_000_000, 100_000_000),
+DP_DEFAULT_WINDOWS = {2: (80_000_000, 200_000_000),
+                      3: (80_000_000, 100_000_000), 4: (80_000_000, 100_000_000),
                       8: (150_000_000, 200_000_000)}
 
 # Wide shards beyond 4 ranks (round 6): at 8 ranks and 7 merges
@@ -415,6 +416,31 @@ def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):
         return False
     lo, hi = win
     return per >= lo and (hi is None or per <= hi)
+
+
+# Small worlds (round 6): the touch divisor damped to k^beta,
+# beta rising with the shard, [(pairs per rank, beta), ...] interpolated
+# linearly in the pairs and clamped at the ends.  2 ranks, once per epoch,
+# target-function gaps A / B at the listed points: 80 M +0.80 / -0.84 %,
+# 100 M +0.58 / -0.67 %, 125 M -0.07 / -0.01 %, 150 M -0.17 / +0.05 %,
+# 200 M +0.10 / +0.57 % (undamped: +0.9..+1.6 / +1.1..+2.6 %)
+DP_BETA_SCHEDULE = {2: [(80_000_000, 1.50), (100_000_000, 1.55), (125_000_000, 1.70),
+                        (150_000_000, 1.75), (200_000_000, 1.85)]}
+
+
+def dp_merge_beta(pairs_per_rank, world, rule="auto"):
+    """the touch divisor's exponent (G2V_OPT_MERGE_BETA_MILLI / 1000) of the
+    auto plan: DP_BETA_SCHEDULE for that world, else 1"""
+    pts = sorted(DP_BETA_SCHEDULE.get(world, ()))
+    if rule != "auto" or not pts:
+        return 1.0
+    x = float(pairs_per_rank)
+    if x <= pts[0][0]:
+        return pts[0][1]
+    for (x0, b0), (x1, b1) in zip(pts, pts[1:]):
+        if x <= x1:
+            return b0 + (b1 - b0) * (x - x0) / (x1 - x0)
+    return pts[-1][1]
 
 
 def dp_merge_plan(pairs_per_rank, merge_every_jobs=None, rule="auto", jobs_per_rank=None,

@@ -260,11 +260,11 @@ def main(argv=None):
                              "this many (any world size); a smaller corpus trains whole on every "
                              "rank (no merges, rank 0 writes).  Default: shard only where the "
                              "merge plan was measured within 1 %% of one model on the target "
-                             "function on both test corpora (DESIGN.md 7a): 3 or 4 ranks with "
-                             "80-100 M pairs per rank, 8 ranks with 150-200 M; never at 2 ranks "
-                             "(+1.1..+2.6 %% there) nor at 5-7 (6 ranks: up to +1.9 %%); C3's 8 x "
-                             "125 M reads -1.1..-1.2 %% on one corpus, 8 x 80 M -4.5 %%.  Setting "
-                             "it is an opt-in to those gaps")
+                             "function on both test corpora (DESIGN.md 7a): 2 ranks with 80-200 M "
+                             "pairs per rank (touch divisor damped to k^beta), 3 or 4 ranks with "
+                             "80-100 M, 8 ranks with 150-200 M; never at 5-7 ranks (6 ranks: up "
+                             "to +1.9 %%); C3's 8 x 125 M reads -1.1..-1.2 %% on one corpus, 8 x "
+                             "80 M -4.5 %%.  Setting it is an opt-in to those gaps")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,
                         help="the pair shuffles (src/gene2vec.py:52,80): 'python' = CPython's "
                              "random.shuffle bit for bit on the host; 'device' = keyed "
@@ -389,9 +389,11 @@ def main(argv=None):
         W.DP_MERGE_RULE, W.DP_MERGE_EVERY_JOBS = Dd.dp_merge_plan(
             n_pairs / max(1, dworld), args.merge_every_jobs, args.merge_rule,
             jobs_per_rank=-(-(-(-n_pairs // max(1, dworld))) // 5000), world=dworld)
+        W.DP_MERGE_BETA = Dd.dp_merge_beta(n_pairs / max(1, dworld), dworld, args.merge_rule)
         if shard:
             print(f"data parallel: {dworld} ranks x {n_pairs // dworld} pairs, {W.DP_MERGE_RULE} "
-                  f"merge every {W.DP_MERGE_EVERY_JOBS} jobs")
+                  f"merge every {W.DP_MERGE_EVERY_JOBS} jobs"
+                  + (f", divisor k^{W.DP_MERGE_BETA:.3f}" if W.DP_MERGE_BETA != 1.0 else ""))
         W.DP_MERGE_TRANSPORT = args.merge_transport
         model = None
         for current_iter in range(1, args.iters + 1):

@@ -304,6 +304,10 @@ DP_MERGE_TRANSPORT = "auto"
 # merge rule of data-parallel training (the CLI picks it by shard size:
 # distributed.dp_merge_plan)
 DP_MERGE_RULE = "touch"
+# touch divisor shape k^beta of the merges (distributed.dp_merge_beta: 1 but
+# at 2 ranks, where the damped divisor keeps the merged model on one model's
+# target function; G2V_OPT_MERGE_BETA_MILLI)
+DP_MERGE_BETA = 1.0
 
 
 def crc32_hash(s):
@@ -384,6 +388,7 @@ class Word2Vec:
         self.grid = int(grid)
         self.merge_every_jobs = DP_MERGE_EVERY_JOBS
         self.merge_rule = DP_MERGE_RULE
+        self.merge_beta = DP_MERGE_BETA
         self.random = np.random.RandomState(seed)
         self.corpus_count = 0
         self.corpus_total_words = 0
@@ -478,6 +483,9 @@ class Word2Vec:
         import torch.distributed as dist
         mode = N.MODE_SEQUENTIAL if self.mode == "sequential" else N.MODE_HOGWILD
         rank, world = dist.get_rank(), dist.get_world_size()
+        beta = float(getattr(self, "merge_beta", 1.0))
+        if beta != 1.0:
+            eng.set_option(N.OPT_MERGE_BETA_MILLI, int(round(beta * 1000)))
         transport = DP_MERGE_TRANSPORT
         if transport == "auto":
             transport = "rccl" if dist.get_backend() == "nccl" else "host"
@@ -507,7 +515,7 @@ class Word2Vec:
         dist.broadcast(tables, src=0)
         eng.bind_tables(tables[0].data_ptr(), tables[1].data_ptr(), eng.ld, keepalive=(tables,))
         self._replica = Dd.ReplicaTrainer(eng, (tables,), self.merge_every_jobs, mode,
-                                          merge=self.merge_rule, backend="torch")
+                                          merge=self.merge_rule, backend="torch", beta=beta)
 
     def _ensure_engine(self):
         if self._engine is not None:
@@ -739,6 +747,7 @@ class Word2Vec:
         m.grid = 0
         m.merge_every_jobs = DP_MERGE_EVERY_JOBS
         m.merge_rule = DP_MERGE_RULE
+        m.merge_beta = DP_MERGE_BETA
         m.total_train_time = 0.0
         m.running_training_loss = float(meta.get("running_training_loss", 0.0))
         m.random = np.random.RandomState()

@@ -1,0 +1,22 @@
+#!/bin/bash
+# round 6 (verdict r5 item 1): 4 ranks with a damped touch divisor k^beta (once per epoch)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+A="--modules 1000 --p-module 0.5 --zipf 1.0"
+B="--modules 600 --p-module 0.3 --zipf 1.2"
+run() {  # pairs every corpus rules tag
+  local P=$1 EV=$2 C=$3 RULES=$4 TAG=$5
+  eval OPTS=\$$C
+  timeout -k 10 400 python -u scripts/replica_quality.py --replicas 4 --pairs-per-replica $P \
+    --iters 10 --ggipnn-repeat 3 $OPTS --merge-every $EV --replica-seeds 1 --single-seeds 1 \
+    --auc-seeds 0 --rules $RULES --out gpurun_out/rq_r06_${TAG}_n4_$C > gpurun_out/r06_rq_${TAG}_n4_$C.log 2>&1 \
+    || { echo "study $TAG $C failed"; tail -20 gpurun_out/r06_rq_${TAG}_n4_$C.log; exit 1; }
+  python3 -c "
+import json; d=json.load(open('gpurun_out/rq_r06_${TAG}_n4_$C/replica_quality.json'))
+for t, r in d['runs'].items(): print('4x$TAG $C', t, {k: r[k] for k in r if k.endswith('gap')})"
+}
+for C in B A; do
+  run 125000000 25100 $C touch:1050:1000,touch:1100:1000 b125 || exit 1
+  run 150000000 30100 $C touch:1100:1000,touch:1150:1000 b150 || exit 1
+done

@@ -82,9 +82,16 @@ def test_default_shard_windows():
     on both test corpora; --dp-min-pairs-per-rank opts in"""
     from gene2vec_amd import distributed as Dd
     M = 1_000_000
-    # 2 ranks: never by default (the merged model leads by 1.1-2.6 % on corpus B)
-    for per in (50 * M, 80 * M, 125 * M, 500 * M):
+    # 2 ranks: 80-200 M pairs per rank with the damped divisor k^beta(shard)
+    for per in (50 * M, 79 * M, 201 * M, 500 * M):
         assert not Dd.dp_default_shard(2 * per, 2)
+    for per in (80 * M, 125 * M, 200 * M):
+        assert Dd.dp_default_shard(2 * per, 2)
+    assert Dd.dp_merge_beta(80 * M, 2) == 1.5 and Dd.dp_merge_beta(125 * M, 2) == 1.7
+    assert abs(Dd.dp_merge_beta(112.5 * M, 2) - 1.625) < 1e-9  # interpolated
+    assert Dd.dp_merge_beta(50 * M, 2) == 1.5 and Dd.dp_merge_beta(300 * M, 2) == 1.85
+    assert Dd.dp_merge_beta(125 * M, 2, rule="touch") == 1.0  # an explicit rule: undamped
+    assert Dd.dp_merge_beta(125 * M, 8) == 1.0
     # 3 and 4 ranks: 80-100 M pairs per rank
     for w in (3, 4):
         assert not Dd.dp_default_shard(w * 79 * M, w)
