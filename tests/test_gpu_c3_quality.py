@@ -17,9 +17,9 @@ Gate (north star: data-parallel quality within 1 % of one model): the
 manuscript target function (src/evaluation_target_function.py, pathways =
 the planted modules), the SGNS objective on training pairs (held-in) and on
 fresh pairs of the generator (held-out), each within 1 %, at points inside
-the CLI's default windows (distributed.DP_DEFAULT_WINDOWS: 3-4 ranks x
-80-100 M pairs per rank, 2 ranks x 80-200 M with a damped divisor, 8
-ranks x 150-200 M) with the plan
+the CLI's default windows (distributed.DP_DEFAULT_WINDOWS: 3 / 4 ranks x
+80-100 M / 80-150 M pairs per rank, 2 ranks x 80-200 M with a damped
+divisor, 8 ranks x 150-200 M) with the plan
 distributed.dp_merge_plan picks there; the last test gates the opt-in plan
 at 8 x 50 M (--dp-min-pairs-per-rank).  Progress goes to
 gpurun_out/c3_quality_progress.log."""
@@ -102,20 +102,21 @@ def test_eight_replicas_wide_shard_within_one_percent_of_one_model(tmp_path):
 @pytest.mark.gpu
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("R,per,corpus", [(4, 100_000_000, "A"), (4, 100_000_000, "B"),
-                                          (3, 80_000_000, "B"), (2, 125_000_000, "B")])
+                                          (3, 80_000_000, "B"), (2, 125_000_000, "B"),
+                                          (4, 150_000_000, "B")])
 def test_small_world_window_within_one_percent_of_one_model(tmp_path, R, per, corpus):
     """the metric's N = 4 point and N = 3 (BASELINE.json: 1/2/4/8 GPUs;
     verdict r5 item 1): R ranks x per pairs inside the CLI's default
-    data-parallel window (distributed.DP_DEFAULT_WINDOWS: 3-4 ranks, 80-100 M
+    data-parallel window (distributed.DP_DEFAULT_WINDOWS: 3 ranks 80-100 M, 4 ranks 80-150 M
     pairs per rank), the plan distributed.dp_merge_plan picks there (touch
     once per epoch), on corpus A (the C3 gate's) and on corpus B (Zipf 1.2,
     600 modules, 30 % rewired), the same gate as the 8-replica test.  Measured
     in round 6: 4 x 100 M +0.07 % (A) / +0.32..+0.43 % (B), 3 x
     80 M B +0.40 % on the target function.  At 2 ranks the plan damps the
     touch divisor to k^beta (distributed.dp_merge_beta: 1.7 at 125 M; 2 x
-    125 M B measured -0.01 %, undamped +2.4..+2.6 %).  At 4 x 125 M corpus B
-    reads +1.30 %: outside the window, the CLI does not shard there by
-    default (tests/test_cli_options.py)."""
+    125 M B measured -0.01 %, undamped +2.4..+2.6 %), and so does 4 ranks
+    from 100 M (1.15 at 150 M: 4 x 150 M B +0.43 %; undamped 4 x 125 M B
+    read +1.30 %)."""
     from gene2vec_amd import distributed as Dd
     from gene2vec_amd import replica_study as RQ
     say = _progress()
