@@ -422,7 +422,9 @@ def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):
 
 # Small worlds (round 6): the touch divisor damped to k^beta,
 # beta rising with the shard, [(pairs per rank, beta), ...] interpolated
-# linearly in the pairs and clamped at the ends.  2 ranks, once per epoch,
+# linearly in the pairs, held at the last point above it, and 1 (undamped)
+# below the first (shards under the default window, which only an explicit
+# --dp-min-pairs-per-rank trains data-parallel).  2 ranks, once per epoch,
 # target-function gaps A / B at the listed points: 80 M +0.80 / -0.84 %,
 # 100 M +0.58 / -0.67 %, 125 M -0.07 / -0.01 %, 150 M -0.17 / +0.05 %,
 # 200 M +0.10 / +0.57 % (undamped: +0.9..+1.6 / +1.1..+2.6 %).  4 ranks:
@@ -440,7 +442,9 @@ def dp_merge_beta(pairs_per_rank, world, rule="auto"):
     if rule != "auto" or not pts:
         return 1.0
     x = float(pairs_per_rank)
-    if x <= pts[0][0]:
+    if x < pts[0][0]:
+        return 1.0  # below the schedule (opt-in small shards): the plain divisor
+    if x == pts[0][0]:
         return pts[0][1]
     for (x0, b0), (x1, b1) in zip(pts, pts[1:]):
         if x <= x1:

@@ -89,7 +89,8 @@ def test_default_shard_windows():
         assert Dd.dp_default_shard(2 * per, 2)
     assert Dd.dp_merge_beta(80 * M, 2) == 1.5 and Dd.dp_merge_beta(125 * M, 2) == 1.7
     assert abs(Dd.dp_merge_beta(112.5 * M, 2) - 1.625) < 1e-9  # interpolated
-    assert Dd.dp_merge_beta(50 * M, 2) == 1.5 and Dd.dp_merge_beta(300 * M, 2) == 1.85
+    assert Dd.dp_merge_beta(300 * M, 2) == 1.85
+    assert Dd.dp_merge_beta(50 * M, 2) == 1.0  # below the window: undamped (opt-in shards)
     assert Dd.dp_merge_beta(125 * M, 2, rule="touch") == 1.0  # an explicit rule: undamped
     assert Dd.dp_merge_beta(125 * M, 8) == 1.0
     # 3 ranks: 80-100 M pairs per rank; 4 ranks: 80-150 M (damped from 100 M)
