@@ -370,7 +370,8 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 #   4 ranks: 80 M -0.36 / -0.63 %, 100 M +0.07 / +0.32..+0.43 %; 125 M reads
 #            +0.33 / +1.30 % undamped (B out): from 100 M the divisor is
 #            damped (DP_BETA_SCHEDULE), 125 M -0.28 / +0.05 %, 150 M
-#            -0.51 / +0.43 %
+#            -0.51 / +0.43 %, 200 M -0.49 / -0.04 %, 250 M -0.57 / -0.11 %
+#            (C3's 1 B pairs over 4)
 #   8 ranks: the wide-shard plan below (touch, DP_WIDE_MERGE_PAIRS / shard
 #            merges per epoch): 150 M (5 per epoch) +0.44 / -0.58 %, 200 M (4)
 #            +0.85 / +0.55 %; 250 M (3) +0.90 / +0.69 % but B's held-in
@@ -390,7 +391,7 @@ DP_EPOCH_MERGE_MAX_WORLD = 4
 # --dp-min-pairs-per-rank (then: shard from that many pairs per rank, any
 # world, with the plan above).
 DP_DEFAULT_WINDOWS = {2: (80_000_000, 200_000_000),
-                      3: (80_000_000, 100_000_000), 4: (80_000_000, 150_000_000),
+                      3: (80_000_000, 100_000_000), 4: (80_000_000, 250_000_000),
                       8: (150_000_000, 200_000_000)}
 
 # Wide shards beyond 4 ranks (round 6): at 8 ranks and 7 merges
@@ -429,10 +430,12 @@ def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):
 # 100 M +0.58 / -0.67 %, 125 M -0.07 / -0.01 %, 150 M -0.17 / +0.05 %,
 # 200 M +0.10 / +0.57 % (undamped: +0.9..+1.6 / +1.1..+2.6 %).  4 ranks:
 # undamped to 100 M (80 M -0.36 / -0.63 %, 100 M +0.07 / +0.32..+0.43 %),
-# 125 M -0.28 / +0.05 %, 150 M -0.51 / +0.43 % (undamped 125 M +0.33 / +1.30 %)
+# 125 M -0.28 / +0.05 %, 150 M -0.51 / +0.43 %, 200 M -0.49 / -0.04 %,
+# 250 M -0.57 / -0.11 % (undamped 125 M +0.33 / +1.30 %)
 DP_BETA_SCHEDULE = {2: [(80_000_000, 1.50), (100_000_000, 1.55), (125_000_000, 1.70),
                         (150_000_000, 1.75), (200_000_000, 1.85)],
-                    4: [(100_000_000, 1.00), (125_000_000, 1.10), (150_000_000, 1.15)]}
+                    4: [(100_000_000, 1.00), (125_000_000, 1.10), (150_000_000, 1.15),
+                        (200_000_000, 1.25), (250_000_000, 1.30)]}
 
 
 def dp_merge_beta(pairs_per_rank, world, rule="auto"):

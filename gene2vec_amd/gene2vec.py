@@ -262,7 +262,7 @@ def main(argv=None):
                              "merge plan was measured within 1 %% of one model on the target "
                              "function on both test corpora (DESIGN.md 7a): 2 ranks with 80-200 M "
                              "pairs per rank (touch divisor damped to k^beta), 3 ranks with "
-                             "80-100 M, 4 with 80-150 M, 8 with 150-200 M; never at 5-7 ranks (6 ranks: up "
+                             "80-100 M, 4 with 80-250 M, 8 with 150-200 M; never at 5-7 ranks (6 ranks: up "
                              "to +1.9 %%); C3's 8 x 125 M reads -1.1..-1.2 %% on one corpus, 8 x "
                              "80 M -4.5 %%.  Setting it is an opt-in to those gaps")
     parser.add_argument("--shuffle", choices=("python", "device"), default=None,

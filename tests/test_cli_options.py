@@ -93,14 +93,15 @@ def test_default_shard_windows():
     assert Dd.dp_merge_beta(50 * M, 2) == 1.0  # below the window: undamped (opt-in shards)
     assert Dd.dp_merge_beta(125 * M, 2, rule="touch") == 1.0  # an explicit rule: undamped
     assert Dd.dp_merge_beta(125 * M, 8) == 1.0
-    # 3 ranks: 80-100 M pairs per rank; 4 ranks: 80-150 M (damped from 100 M)
-    for w, hi in ((3, 100), (4, 150)):
+    # 3 ranks: 80-100 M pairs per rank; 4 ranks: 80-250 M (damped from 100 M)
+    for w, hi in ((3, 100), (4, 250)):
         assert not Dd.dp_default_shard(w * 79 * M, w)
         assert Dd.dp_default_shard(w * 80 * M, w) and Dd.dp_default_shard(w * hi * M, w)
         assert not Dd.dp_default_shard(w * (hi + 1) * M, w)
     assert Dd.dp_default_shard(4 * 125 * M, 4) and not Dd.dp_default_shard(3 * 125 * M, 3)
     assert Dd.dp_merge_beta(90 * M, 4) == 1.0 and Dd.dp_merge_beta(125 * M, 4) == 1.1
     assert Dd.dp_merge_beta(150 * M, 4) == 1.15 and Dd.dp_merge_beta(100 * M, 3) == 1.0
+    assert Dd.dp_merge_beta(250 * M, 4) == 1.3 and Dd.dp_default_shard(10 ** 9, 4)  # C3 over 4
     # 5-7 ranks: never by default; 8 ranks with 150-200 M pairs per rank (not
     # C3's 125 M, where corpus B reads -1.1..-1.2 %)
     for w in (5, 6, 7):

@@ -18,7 +18,7 @@ manuscript target function (src/evaluation_target_function.py, pathways =
 the planted modules), the SGNS objective on training pairs (held-in) and on
 fresh pairs of the generator (held-out), each within 1 %, at points inside
 the CLI's default windows (distributed.DP_DEFAULT_WINDOWS: 3 / 4 ranks x
-80-100 M / 80-150 M pairs per rank, 2 ranks x 80-200 M with a damped
+80-100 M / 80-250 M pairs per rank, 2 ranks x 80-200 M with a damped
 divisor, 8 ranks x 150-200 M) with the plan
 distributed.dp_merge_plan picks there; the last test gates the opt-in plan
 at 8 x 50 M (--dp-min-pairs-per-rank).  Progress goes to
@@ -107,7 +107,7 @@ def test_eight_replicas_wide_shard_within_one_percent_of_one_model(tmp_path):
 def test_small_world_window_within_one_percent_of_one_model(tmp_path, R, per, corpus):
     """the metric's N = 4 point and N = 3 (BASELINE.json: 1/2/4/8 GPUs;
     verdict r5 item 1): R ranks x per pairs inside the CLI's default
-    data-parallel window (distributed.DP_DEFAULT_WINDOWS: 3 ranks 80-100 M, 4 ranks 80-150 M
+    data-parallel window (distributed.DP_DEFAULT_WINDOWS: 3 ranks 80-100 M, 4 ranks 80-250 M
     pairs per rank), the plan distributed.dp_merge_plan picks there (touch
     once per epoch), on corpus A (the C3 gate's) and on corpus B (Zipf 1.2,
     600 modules, 30 % rewired), the same gate as the 8-replica test.  Measured
