@@ -428,7 +428,9 @@ def dp_default_shard(n_pairs, world, min_pairs_per_rank=None):
 # --dp-min-pairs-per-rank trains data-parallel).  2 ranks, once per epoch,
 # target-function gaps A / B at the listed points: 80 M +0.80 / -0.84 %,
 # 100 M +0.58 / -0.67 %, 125 M -0.07 / -0.01 %, 150 M -0.17 / +0.05 %,
-# 200 M +0.10 / +0.57 % (undamped: +0.9..+1.6 / +1.1..+2.6 %).  4 ranks:
+# 200 M +0.10 / +0.57 % (undamped: +0.9..+1.6 / +1.1..+2.6 %; past 200 M no
+# beta measured holds B: 300 M beta 2.0 +0.12 / +1.49 %, 500 M beta 2.15
+# +1.08 / +1.07 %, so the 2-rank window ends at 200 M).  4 ranks:
 # undamped to 100 M (80 M -0.36 / -0.63 %, 100 M +0.07 / +0.32..+0.43 %),
 # 125 M -0.28 / +0.05 %, 150 M -0.51 / +0.43 %, 200 M -0.49 / -0.04 %,
 # 250 M -0.57 / -0.11 % (undamped 125 M +0.33 / +1.30 %)
