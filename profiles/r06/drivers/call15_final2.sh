@@ -3,7 +3,7 @@
 # driver's command), and the strong-scaling leg at N = 1 (1 B pairs on one GPU)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r06final4
+O=gpurun_out/r06final5
 mkdir -p $O
 # the counters this gfx950 exposes (looking for an Infinity-Cache / HBM split)
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
