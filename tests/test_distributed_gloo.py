@@ -399,3 +399,59 @@ def test_gather_corpus_declines_non_pairs(tmp_path):
     p1.write_text("G00001 G00002 G00003\n", encoding="windows-1252")
     res = _run_gather([p0, str(p1)], 2)
     assert res[0] is None and res[1] is None
+
+
+class _OptEngine:
+    """records set_option / comm_init_host calls (libg2v-backend stand-in)"""
+
+    def __init__(self):
+        self.opts, self.host = {}, None
+
+    def set_option(self, k, v):
+        self.opts[k] = v
+
+    def comm_init_host(self, hc, world, rank):
+        self.host = (world, rank)
+
+
+def _bind_worker(rank, world, port, betas, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from types import SimpleNamespace
+
+    from gene2vec_amd import _native as N
+    from gene2vec_amd import word2vec as W
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out = []
+        for beta in betas:
+            me = SimpleNamespace(mode="hogwild", merge_beta=beta, merge_every_jobs=100,
+                                 merge_rule="touch")
+            eng = _OptEngine()
+            W.Word2Vec._bind_replica(me, eng)
+            out.append((eng.opts.get(N.OPT_MERGE_BETA_MILLI), eng.host,
+                        me._replica.avg_every_jobs, me._replica.merge))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bind_replica_sets_the_plans_merge_beta():
+    """the CLI's damped divisor (distributed.dp_merge_beta)
+    reaches libg2v: Word2Vec._bind_replica sets G2V_OPT_MERGE_BETA_MILLI on
+    every rank's engine when the plan damps (beta != 1), and leaves the
+    library default otherwise; world size 2 over gloo (the host transport)"""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bind_worker, args=(r, 2, port, (1.7, 1.0), q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank in (0, 1):
+        damped, plain = res[rank]
+        assert damped == (1700, (2, rank), 100, "touch")
+        assert plain == (None, (2, rank), 100, "touch")
